@@ -1,0 +1,387 @@
+"""CPU oracle for the CiM partial-sum-quantized convolution.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (``cim_quantization_amd``)
+imports, links or executes this module; only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg use it, as the checker / CPU baseline.
+
+This is a from-scratch numpy restatement of the reference algorithm in
+``models/_modules/lsq.py`` (UtkarshSaxena1/CiM_Quantization @ 2024-10-22).  It follows
+the reference's fp32 op sequence step by step -- including its numerical artefacts
+(the non-integer ``x_q/sa`` round trip, int8 truncation/wrap of the saved context,
+the fp16 partial-sum store, the int8 wrap of ``binary_mask``) -- because the
+GPU path has to be bit-exact with the reference on the integer steps.
+
+Parity of this oracle is pinned against the real reference: ``tests/golden/
+make_golden.py`` imports the reference (this container only), runs it on seeded
+inputs, asserts this oracle agrees, and commits the vectors under ``tests/golden``.
+
+Layout conventions (all identical to the reference):
+  x           [B, C, H, W]  fp32 (NCHW)
+  weight      [O, C, k, k]  fp32
+  unfold      [B, P, K]     P = Ho*Wo, K = C*k*k, f = c*k*k + kh*k + kw
+  ps (fp16)   [B, T, nbw, nba, P, O]
+  alpha_cim   [1, T, nbw, nba, 1, O]
+  out         [B, P, O]
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+F32 = np.float32
+F16 = np.float16
+
+
+# ----------------------------------------------------------------------------------------
+# scalar helpers (lsq.py:23-32)
+# ----------------------------------------------------------------------------------------
+def grad_scale_value(alpha, scale: float) -> np.ndarray:
+    """Value of ``grad_scale(alpha, scale)`` (lsq.py:23-26): ``(a - a*s) + a*s`` in fp32.
+
+    The python-double ``scale`` is rounded to fp32 before the multiply, as torch does
+    for a wrapped scalar operand of a float32 tensor op.  The value may differ from
+    ``alpha`` by one ulp."""
+    a = np.asarray(alpha, dtype=F32)
+    ag = (a * F32(scale)).astype(F32)
+    return ((a - ag).astype(F32) + ag).astype(F32)
+
+
+def round_pass_value(v: np.ndarray) -> np.ndarray:
+    """Value of ``round_pass(v)`` (lsq.py:29-32): ``(rint(v) - v) + v`` in fp32."""
+    v = np.asarray(v, dtype=F32)
+    r = np.rint(v).astype(F32)
+    return ((r - v).astype(F32) + v).astype(F32)
+
+
+def to_int8(x: np.ndarray) -> np.ndarray:
+    """``tensor.type(torch.int8)`` on the CPU: truncate toward zero, wrap mod 256."""
+    t = np.trunc(np.asarray(x, dtype=np.float64))
+    t = np.nan_to_num(t, nan=0.0, posinf=0.0, neginf=0.0).astype(np.int64)
+    return (t & 0xFF).astype(np.uint8).view(np.int8)
+
+
+def remainder(a: np.ndarray, b: float) -> np.ndarray:
+    """``torch.remainder`` for float tensors: fmod, then shift into the divisor's sign."""
+    a = np.asarray(a, dtype=F32)
+    b = F32(b)
+    mod = np.fmod(a, b).astype(F32)
+    fix = (mod != 0) & ((b < 0) != (mod < 0))
+    mod = np.where(fix, (mod + b).astype(F32), mod)
+    return mod.astype(F32)
+
+
+# ----------------------------------------------------------------------------------------
+# LSQ quantisers (lsq.py:537-555) and alpha_cim quantisation (lsq.py:566-573)
+# ----------------------------------------------------------------------------------------
+def lsq_act_params(nbits_a: int):
+    """Activation range: Qn=0, Qp=2^b-1, even for signed inputs (lsq.py:537-538)."""
+    return 0, 2 ** nbits_a - 1
+
+
+def lsq_weight_params(nbits_w: int):
+    """Weight range: Qn=-2^(b-1), Qp=2^(b-1)-1 (lsq.py:523-524)."""
+    return -(2 ** (nbits_w - 1)), 2 ** (nbits_w - 1) - 1
+
+
+def lsq_quantize(x: np.ndarray, scale: np.ndarray, qn: float, qp: float):
+    """``round_pass(clamp(x/s, qn, qp)) * s`` (lsq.py:549 / :555).
+
+    Returns (x_q, codes) with codes = rint(clamp(x/s)) (clamp before round)."""
+    s = np.asarray(scale, dtype=F32).reshape(-1)[:1]
+    v = (np.asarray(x, dtype=F32) / s).astype(F32)
+    c = np.clip(v, F32(qn), F32(qp)).astype(F32)
+    r = round_pass_value(c)
+    return (r * s).astype(F32), r
+
+
+def alpha_quantize(alpha: np.ndarray, nbits_alpha: int) -> np.ndarray:
+    """8-bit uniform quantisation of alpha_cim (lsq.py:566-571).
+
+    scale = (max - min)/(2^b - 2); alpha_q = clamp(round_pass(alpha/scale), 1, 2^b-1)*scale.
+    All-equal alphas give scale 0 and a NaN alpha_q (inf - inf inside round_pass)."""
+    a = np.asarray(alpha, dtype=F32)
+    qp, qn = 2 ** nbits_alpha - 1, 1
+    with np.errstate(all="ignore"):
+        scale = ((a.max() - a.min()).astype(F32) / F32(qp - qn)).astype(F32)
+        q = round_pass_value((a / scale).astype(F32))
+        q = np.clip(q, F32(qn), F32(qp)).astype(F32)
+        return (q * scale).astype(F32)
+
+
+def make_binary_mask(nbw: int, nba: int, wbs: int, abs_: int) -> np.ndarray:
+    """``_Conv2dQCiM.binary_mask`` (_quan_base.py:207-214): int8(2^(abs*j) * 2^(wbs*k))
+    with shape [1,1,nbw,nba,1,1]; the int8 cast wraps for 8-bit layers."""
+    m = np.empty((nbw, nba), dtype=np.float64)
+    for j in range(nba):
+        for k in range(nbw):
+            m[k, j] = float((2 ** abs_) ** j) * float((2 ** wbs) ** k)
+    return to_int8(m).reshape(1, 1, nbw, nba, 1, 1)
+
+
+# ----------------------------------------------------------------------------------------
+# im2col / col2im (nn.Unfold / nn.Fold as used at lsq.py:141, :290, :382)
+# ----------------------------------------------------------------------------------------
+def out_size(h: int, k: int, pad: int, stride: int) -> int:
+    return (h + 2 * pad - k) // stride + 1
+
+
+def unfold(x: np.ndarray, k: int, padding, stride) -> np.ndarray:
+    """im2col: [B,C,H,W] -> [B, P, C*k*k] (rows = output pixels, row-major)."""
+    b, c, h, w = x.shape
+    ph, pw = padding
+    sh, sw_ = stride
+    ho, wo = out_size(h, k, ph, sh), out_size(w, k, pw, sw_)
+    xp = np.zeros((b, c, h + 2 * ph, w + 2 * pw), dtype=x.dtype)
+    xp[:, :, ph:ph + h, pw:pw + w] = x
+    cols = np.empty((b, c, k, k, ho, wo), dtype=x.dtype)
+    for kh in range(k):
+        for kw in range(k):
+            cols[:, :, kh, kw] = xp[:, :, kh:kh + sh * (ho - 1) + 1:sh, kw:kw + sw_ * (wo - 1) + 1:sw_]
+    return cols.reshape(b, c * k * k, ho * wo).transpose(0, 2, 1)
+
+
+def fold(cols: np.ndarray, hw, k: int, padding, stride) -> np.ndarray:
+    """col2im: [B, C*k*k, P] -> [B,C,H,W], summing overlapping patches."""
+    b, kk, p = cols.shape
+    h, w = hw
+    ph, pw = padding
+    sh, sw_ = stride
+    c = kk // (k * k)
+    ho, wo = out_size(h, k, ph, sh), out_size(w, k, pw, sw_)
+    assert ho * wo == p
+    cv = cols.reshape(b, c, k, k, ho, wo)
+    xp = np.zeros((b, c, h + 2 * ph, w + 2 * pw), dtype=cols.dtype)
+    for kh in range(k):
+        for kw in range(k):
+            xp[:, :, kh:kh + sh * (ho - 1) + 1:sh, kw:kw + sw_ * (wo - 1) + 1:sw_] += cv[:, :, kh, kw]
+    return xp[:, :, ph:ph + h, pw:pw + w]
+
+
+# ----------------------------------------------------------------------------------------
+# bit slicing (lsq.py:438-509)
+# ----------------------------------------------------------------------------------------
+def _slice_planes(t: np.ndarray, n: int, bs: int) -> np.ndarray:
+    """Digit extraction on a [..., n, ...]-repeated tensor along axis -? (caller picks).
+    ``t`` has the slice axis first. floor(t/2^(bs*i)) for i>=1, then remainder 2^bs."""
+    t = t.astype(F32).copy()
+    for i in range(1, n):
+        t[i] = np.floor((t[i] / F32((2 ** bs) ** i)).astype(F32)).astype(F32)
+    return remainder(t, 2 ** bs)
+
+
+def slicing_act(x: np.ndarray, bits: int, bs: int) -> np.ndarray:
+    """Unsigned act slicing (lsq.py:466-480): [n, *x.shape], LSB first."""
+    n = int(bits / bs)
+    t = np.repeat(np.asarray(x, F32)[None], n, axis=0)
+    return _slice_planes(t, n, bs)
+
+
+def _split_pos_neg(x: np.ndarray):
+    x = np.asarray(x, F32)
+    pos = np.where(x <= 0, F32(0), x).astype(F32)
+    neg = np.where(x >= 0, F32(0), x).astype(F32)
+    return pos, (F32(-1) * neg).astype(F32)
+
+
+def slicing_signed(x: np.ndarray, bits: int, bs: int) -> np.ndarray:
+    """Signed slicing used for weights (lsq.py:438-464) and signed activations
+    (lsq.py:483-509): slice the positive and negated-negative parts, subtract."""
+    n = int(bits / bs)
+    pos, neg = _split_pos_neg(x)
+    sp = _slice_planes(np.repeat(pos[None], n, axis=0), n, bs)
+    sn = _slice_planes(np.repeat(neg[None], n, axis=0), n, bs)
+    return (sp - sn).astype(F32)
+
+
+# ----------------------------------------------------------------------------------------
+# ADC (lsq.py:125-131, :195-230)
+# ----------------------------------------------------------------------------------------
+def adc_range(adc_bits):
+    if adc_bits == 1 or adc_bits == 1.5:
+        return -1, 1
+    return -1 * (2 ** (adc_bits - 1)), (2 ** (adc_bits - 1)) - 1
+
+
+def _tiles(K: int, arr: int):
+    """Crossbar tiles of the flattened dim: full tiles then one remainder (lsq.py:166-185)."""
+    full = K // arr
+    t = [(i * arr, (i + 1) * arr) for i in range(full)]
+    if K % arr:
+        t.append((full * arr, K))
+    return t
+
+
+class CimCtx:
+    """What the reference saves for backward (lsq.py:99-192)."""
+
+
+def cim_forward(x_q, w_q, stride, padding, dilation, act_bits, act_bs, w_bits, w_bs,
+                adc_bits, arr, binary_mask, alpha_cim, sw, sa, stochastic=False,
+                signed_act=0.0, return_debug=False):
+    """``get_cim_output_signed.forward`` (lsq.py:92-237). Returns out [B, P, O] fp32
+    and the saved context (int8 x_int, int8 weight slices, fp16 partial sums)."""
+    if stochastic:
+        raise NotImplementedError("stochastic ADC is statistical; no bit-exact oracle")
+    x_q = np.asarray(x_q, F32)
+    w_q = np.asarray(w_q, F32)
+    sa = np.asarray(sa, F32).reshape(1)
+    sw = np.asarray(sw, F32).reshape(1)
+    x_int = (x_q / sa).astype(F32)                                   # :97
+    w_int = (w_q / sw).astype(F32)                                   # :98
+    ctx = CimCtx()
+    ctx.x_int8 = to_int8(x_int)                                      # :99
+    nbw, nba = int(w_bits / w_bs), int(act_bits / act_bs)            # :115-117
+    O, C, k = w_int.shape[0], w_int.shape[1], w_int.shape[2]
+    fold_x = int((x_int.shape[-1] - w_int.shape[-1] + 2 * padding[0]) / stride[0] + 1)  # :123
+    qn, qp = adc_range(adc_bits)
+    x_unf = unfold(x_int, k, padding, stride)                        # :141
+    B, P, K = x_unf.shape
+    assert P == fold_x * fold_x, "reference assumes square outputs"
+    if float(np.asarray(signed_act).reshape(-1)[0]) != 0:            # :146-149
+        xs = slicing_signed(x_unf, act_bits, act_bs).transpose(1, 0, 2, 3)
+    else:
+        xs = slicing_act(x_unf, act_bits, act_bs).transpose(1, 0, 2, 3)
+    w_unf = w_int.reshape(O, -1).T                                   # :153
+    ws = slicing_signed(w_unf, w_bits, w_bs)                         # :155  [nbw, K, O]
+    ctx.w_sliced8 = to_int8(ws)                                      # :160
+    tiles = _tiles(K, arr)
+    T = math.ceil(K / arr)                                           # :166
+    ps = np.empty((B, T, nbw, nba, P, O), dtype=F16)                 # :169
+    for i, (lo, hi) in enumerate(tiles):                             # :172-185
+        for j in range(nba):
+            for kk in range(nbw):
+                ps[:, i, kk, j] = np.matmul(xs[:, j, :, lo:hi], ws[kk, lo:hi, :]).astype(F16)
+    ctx.ps16 = ps                                                    # :192
+    u = ((ps.astype(F32) * sw).astype(F32) * sa).astype(F32)         # :195
+    with np.errstate(all="ignore"):
+        if adc_bits == 0:                                            # :197
+            adc = u
+        elif adc_bits == 1:                                          # :200
+            adc = (np.sign(u) * np.asarray(alpha_cim, F32)).astype(F32)
+        elif adc_bits == 1.5:                                        # :223-225
+            a = np.asarray(alpha_cim, F32)
+            adc = np.clip(np.rint((u / a).astype(F32)), F32(qn), F32(qp)).astype(F32)
+            adc = (adc * a).astype(F32)
+        else:                                                        # :228-230
+            sws = (sw * sa).astype(F32)
+            adc = np.clip(np.rint((u / sws).astype(F32)), F32(qn), F32(qp)).astype(F32)
+            adc = ((adc * sw).astype(F32) * sa).astype(F32)
+    out = np.sum((adc * binary_mask.astype(F32)).astype(F32), axis=(1, 2, 3), dtype=F32)  # :233
+    ctx.meta = dict(stride=tuple(stride), padding=tuple(padding), k=k, C=C, O=O, H=x_q.shape[2],
+                    W=x_q.shape[3], nbw=nbw, nba=nba, w_bs=w_bs, act_bs=act_bs, act_bits=act_bits,
+                    adc_bits=adc_bits, arr=arr, T=T, K=K, P=P, B=B, qn=qn, qp=qp)
+    ctx.sw, ctx.sa = sw, sa
+    ctx.alpha = None if alpha_cim is None else np.asarray(alpha_cim, F32)
+    ctx.binary_mask = binary_mask
+    ctx.signed_act = float(np.asarray(signed_act).reshape(-1)[0])
+    if return_debug:
+        ctx.x_int, ctx.xs, ctx.ws, ctx.u, ctx.adc = x_int, xs, ws, u, adc
+    return out.astype(F32), ctx
+
+
+def cim_backward(ctx: CimCtx, grad_out: np.ndarray, absolute: bool = False):
+    """``get_cim_output_signed.backward`` (lsq.py:244-386).
+
+    Returns (grad_x [B,C,H,W], grad_w [O,C,k,k], grad_alpha [1,T,nbw,nba,1,O] or None).
+    ``absolute=True`` re-runs the same contraction in fp64 on |operands|, giving the
+    per-element sum of |terms| that the parity tolerances are scaled by."""
+    m = ctx.meta
+    dt = np.float64 if absolute else F32
+    A = (np.abs if absolute else (lambda v: v))
+    sw, sa = ctx.sw.astype(dt), ctx.sa.astype(dt)
+    nbw, nba, T, K, P, B, O = m["nbw"], m["nba"], m["T"], m["K"], m["P"], m["B"], m["O"]
+    w_sl = (ctx.w_sliced8.astype(dt) * sw).astype(dt)                # :249-252
+    x_int = ctx.x_int8.astype(dt)                                    # :253
+    adc_bits = m["adc_bits"]
+    with np.errstate(all="ignore"):
+        # the clamp masks and ADC codes are decided in fp32 even for the |terms| pass
+        if adc_bits in (1, 1.5):                                     # :257-264
+            ps = ((ctx.ps16.astype(F32) * ctx.sw).astype(F32) * ctx.sa).astype(F32)
+            ps = (ps / ctx.alpha).astype(F32)
+        else:
+            ps = ctx.ps16.astype(F32)
+    x_unf = unfold(x_int, m["k"], m["padding"], m["stride"])         # :290
+    if ctx.signed_act:                                               # :291-295
+        xs = slicing_signed(x_unf, m["act_bits"], m["act_bs"]).transpose(1, 0, 2, 3)
+    else:
+        xs = slicing_act(x_unf, m["act_bits"], m["act_bs"]).transpose(1, 0, 2, 3)
+    xs = (xs.astype(dt) * sa).astype(dt)
+    g = np.asarray(grad_out, dt)
+    G = np.broadcast_to(g[:, None, None, None], (B, T, nbw, nba, P, O))          # :301
+    G = (G * ctx.binary_mask.astype(dt)).astype(dt)                              # :306
+    G_after = G.copy()                                                           # :307
+    thr_hi = F32(m["qp"] + 1e-5)
+    thr_lo = F32(m["qn"] - 1e-5)
+    greater = ps >= thr_hi                                                       # :310
+    lesser = ps <= thr_lo                                                        # :311
+    Gm = np.where(greater | lesser, dt(0), G).astype(dt)                         # :313
+    grad_alpha = None
+    numel = ps.size
+    c = F32(1.0 / math.sqrt(numel * m["qp"])) if adc_bits in (1, 1.5) else None
+    if adc_bits == 1:                                                            # :321-325
+        q = np.sign(ps).astype(dt)
+        terms = ((A(q) * c).astype(dt) * A(G_after)).astype(dt)
+        grad_alpha = np.sum(terms, axis=(0, 4), keepdims=True)
+    elif adc_bits == 1.5:                                                        # :326-332
+        q = np.rint(ps).astype(dt)
+        q = np.where(greater, dt(m["qp"]), q)
+        q = np.where(lesser, dt(m["qn"]), q)
+        terms = ((A(q) * c).astype(dt) * A(G_after)).astype(dt)
+        grad_alpha = np.sum(terms, axis=(0, 4), keepdims=True)
+    gi = np.empty((B, nbw, nba, P, K), dt)                                       # :336
+    gw = np.empty((nbw, nba, K, O), dt)                                          # :337
+    for i, (lo, hi) in enumerate(_tiles(K, m["arr"])):                           # :338-356
+        for j in range(nba):
+            xt = A(xs[:, j, :, lo:hi]).transpose(0, 2, 1)
+            for kk in range(nbw):
+                gt = A(Gm[:, i, kk, j])
+                gi[:, kk, j, :, lo:hi] = np.matmul(gt, A(w_sl[kk, lo:hi, :]).T)
+                gw[kk, j, lo:hi, :] = np.matmul(xt, gt).sum(0)
+    gw = gw.sum(axis=1)                                                          # :362
+    for i in range(1, nbw):                                                      # :363-364
+        gw[i] = gw[i] / dt((2 ** m["w_bs"]) ** i)
+    gw = gw.mean(axis=0, dtype=dt).astype(dt)                                    # :366
+    C, k = m["C"], m["k"]
+    gw = np.ascontiguousarray(gw.T).reshape(O, C, k, k)                          # :369
+    gi = gi.sum(axis=1)                                                          # :372
+    for i in range(1, nba):                                                      # :373-374
+        gi[:, i] = gi[:, i] / dt((2 ** m["act_bs"]) ** i)
+    gi = gi.mean(axis=1, dtype=dt).astype(dt)                                    # :376
+    gx = fold(gi.transpose(0, 2, 1), (m["H"], m["W"]), k, m["padding"], m["stride"])  # :380-382
+    return gx.astype(dt), gw.astype(dt), (None if grad_alpha is None else grad_alpha.astype(dt))
+
+
+# ----------------------------------------------------------------------------------------
+# alpha_cim initialisation path (lsq.py:35-87 and :557-563)
+# ----------------------------------------------------------------------------------------
+def analog_partial_sums(x_q, w_q, stride, padding, act_bits, act_bs, w_bits, w_bs, arr, sw, sa):
+    """``get_analog_partial_sums_signed`` (lsq.py:35-87): fp32 partial sums times sw*sa,
+    activations always sliced unsigned (:51)."""
+    sa = np.asarray(sa, F32).reshape(1)
+    sw = np.asarray(sw, F32).reshape(1)
+    w_int = (np.asarray(w_q, F32) / sw).astype(F32)
+    x_int = (np.asarray(x_q, F32) / sa).astype(F32)
+    nbw, nba = int(w_bits / w_bs), int(act_bits / act_bs)
+    O, k = w_int.shape[0], w_int.shape[2]
+    x_unf = unfold(x_int, k, padding, stride)
+    B, P, K = x_unf.shape
+    xs = slicing_act(x_unf, act_bits, act_bs).transpose(1, 0, 2, 3)
+    ws = slicing_signed(w_int.reshape(O, -1).T, w_bits, w_bs)
+    T = math.ceil(K / arr)
+    ps = np.empty((B, T, nbw, nba, P, O), F32)
+    for i, (lo, hi) in enumerate(_tiles(K, arr)):
+        for j in range(nba):
+            for kk in range(nbw):
+                ps[:, i, kk, j] = np.matmul(xs[:, j, :, lo:hi], ws[kk, lo:hi, :])
+    return ((ps * sw).astype(F32) * sa).astype(F32)
+
+
+def alpha_cim_init(x_q, w_q, stride, padding, act_bits, act_bs, w_bits, w_bs, arr, sw, sa, adc_bits):
+    """alpha_cim = 2*mean_{b,p}|ps*sw*sa|/sqrt(Qp_adc), zeros replaced by sw*sa (lsq.py:557-563)."""
+    qn, qp = adc_range(adc_bits)
+    u = analog_partial_sums(x_q, w_q, stride, padding, act_bits, act_bs, w_bits, w_bs, arr, sw, sa)
+    t = (F32(2.0) * np.abs(u).mean(axis=(0, 4), keepdims=True, dtype=F32)).astype(F32)
+    t = (t / F32(math.sqrt(qp))).astype(F32)
+    fill = (np.asarray(sw, F32).reshape(1) * F32(1.0)).astype(F32) * np.asarray(sa, F32).reshape(1)
+    return np.where(t == 0, fill.astype(F32), t).astype(F32)
