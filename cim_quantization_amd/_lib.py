@@ -1,0 +1,166 @@
+"""ctypes binding of libcimq.so (the C ABI declared in include/cimq.h).
+
+The shared library is built in-tree (``python -m cim_quantization_amd.build`` or
+``__graft_entry__.build()``) and loaded from this package directory.  There is no
+fallback: if the library is missing or was built for another ABI, every compute entry
+point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcimq.so")
+ABI_VERSION = 1
+
+CIMQ_INPUT_XQ = 0
+CIMQ_INPUT_RAW_LSQ = 1
+
+# every symbol include/cimq.h declares
+EXPORTED_SYMBOLS = (
+    "cimq_abi_version",
+    "cimq_last_error",
+    "cimq_query_sizes",
+    "cimq_forward",
+    "cimq_backward",
+    "cimq_alpha_init",
+    "cimq_debug_partial_sums",
+    "cimq_profile_start",
+    "cimq_profile_stop",
+)
+
+KERNEL_IDS = {"fwd": 1, "bwd_gx": 2, "bwd_gw": 3, "prep_act": 4}
+KERNEL_SYMBOLS = {1: "cim_fwd_kernel", 2: "cim_bwd_gx_kernel", 3: "cim_bwd_gw_kernel", 4: "prep_act_kernel"}
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of ``cimq_conv_desc``."""
+
+    _fields_ = [
+        ("batch", ctypes.c_int32), ("in_channels", ctypes.c_int32),
+        ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32),
+        ("out_channels", ctypes.c_int32), ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32),
+        ("stride_h", ctypes.c_int32), ("stride_w", ctypes.c_int32),
+        ("pad_h", ctypes.c_int32), ("pad_w", ctypes.c_int32),
+        ("xbar", ctypes.c_int32),
+        ("bits_w", ctypes.c_int32), ("bits_a", ctypes.c_int32),
+        ("bs_w", ctypes.c_int32), ("bs_a", ctypes.c_int32),
+        ("adc_bits", ctypes.c_float),
+        ("input_kind", ctypes.c_int32),
+        ("lsq_qp", ctypes.c_float),
+        ("reserved", ctypes.c_int32 * 4),
+    ]
+
+
+class Sizes(ctypes.Structure):
+    """Mirror of ``cimq_sizes``."""
+
+    _fields_ = [("ctx_bytes", ctypes.c_size_t), ("fwd_workspace_bytes", ctypes.c_size_t),
+                ("bwd_workspace_bytes", ctypes.c_size_t)]
+
+
+_VP = ctypes.c_void_p
+_lock = threading.Lock()
+_lib = None
+
+
+class CimqError(RuntimeError):
+    pass
+
+
+def _bind(lib):
+    lib.cimq_abi_version.restype = ctypes.c_int
+    lib.cimq_abi_version.argtypes = []
+    lib.cimq_last_error.restype = ctypes.c_char_p
+    lib.cimq_last_error.argtypes = []
+    lib.cimq_query_sizes.restype = ctypes.c_int
+    lib.cimq_query_sizes.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(Sizes)]
+    lib.cimq_forward.restype = ctypes.c_int
+    lib.cimq_forward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 11
+    lib.cimq_backward.restype = ctypes.c_int
+    lib.cimq_backward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 14
+    lib.cimq_alpha_init.restype = ctypes.c_int
+    lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
+    lib.cimq_debug_partial_sums.restype = ctypes.c_int
+    lib.cimq_debug_partial_sums.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
+    lib.cimq_profile_start.restype = ctypes.c_int
+    lib.cimq_profile_start.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.cimq_profile_stop.restype = ctypes.c_int
+    lib.cimq_profile_stop.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    return lib
+
+
+def load(path: str | None = None):
+    """Load (once) and return the bound library; raises CimqError if unavailable."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise CimqError(f"libcimq.so not found at {p}; build it with "
+                            f"`python -m cim_quantization_amd.build` (hipcc --offload-arch=gfx950)")
+        lib = _bind(ctypes.CDLL(p))
+        v = lib.cimq_abi_version()
+        if v != ABI_VERSION:
+            raise CimqError(f"libcimq ABI {v} != expected {ABI_VERSION}; rebuild")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().cimq_last_error().decode(errors="replace")
+        raise CimqError(f"{what} failed (status {rc}): {msg}")
+
+
+def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w, bs_a, adc_bits,
+              input_kind=CIMQ_INPUT_XQ, lsq_qp=0.0) -> ConvDesc:
+    d = ConvDesc()
+    d.batch, d.in_channels, d.in_h, d.in_w = int(B), int(C), int(H), int(W)
+    d.out_channels, d.kernel_h, d.kernel_w = int(O), int(KH), int(KW)
+    d.stride_h, d.stride_w = int(stride[0]), int(stride[1])
+    d.pad_h, d.pad_w = int(padding[0]), int(padding[1])
+    d.xbar = int(xbar)
+    d.bits_w, d.bits_a, d.bs_w, d.bs_a = int(bits_w), int(bits_a), int(bs_w), int(bs_a)
+    d.adc_bits = float(adc_bits)
+    d.input_kind = int(input_kind)
+    d.lsq_qp = float(lsq_qp)
+    return d
+
+
+def query_sizes(desc: ConvDesc) -> Sizes:
+    s = Sizes()
+    check(load().cimq_query_sizes(ctypes.byref(desc), ctypes.byref(s)), "cimq_query_sizes")
+    return s
+
+
+class KernelTimer:
+    """Sum of HIP-event-measured durations of every launch of one libcimq kernel."""
+
+    def __init__(self, kernel: str, max_launches: int = 65536):
+        self.kid = KERNEL_IDS[kernel]
+        self.cap = max_launches
+        self.total_ms = 0.0
+        self.launches = 0
+        self.algo_bytes = 0.0
+        self.algo_flops = 0.0
+
+    def __enter__(self):
+        check(load().cimq_profile_start(self.kid, self.cap), "cimq_profile_start")
+        return self
+
+    def __exit__(self, *exc):
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        b, f = ctypes.c_double(), ctypes.c_double()
+        check(load().cimq_profile_stop(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), ctypes.byref(f)),
+              "cimq_profile_stop")
+        self.total_ms, self.launches = ms.value, n.value
+        self.algo_bytes, self.algo_flops = b.value, f.value
+        return False

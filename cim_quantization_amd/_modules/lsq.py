@@ -1,0 +1,171 @@
+"""LSQ and CiM quantised modules -- MI355X drop-in for models/_modules/lsq.py.
+
+``Conv2dLSQCiM`` keeps the reference's constructor, parameters, buffers, first-step
+initialisation and output layout, and runs the quantised conv on libcimq's HIP kernels:
+the activation quantiser is fused into the CiM kernels (x_q is never materialised), the
+partial sums are integer MFMA products, the ADC is applied from exact integer thresholds.
+``get_cim_output_signed`` is re-exported with the reference's 17-argument signature.
+
+``Conv2dLSQ`` / ``LinearLSQ`` / ``ActLSQ`` (plain LSQ fake-quant, unused by the CiM
+example, SURVEY.md section 8f "next") are provided with the reference's semantics on
+torch device ops.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ..functional import alpha_cim_init, cim_conv2d_lsq, get_cim_output_signed  # noqa: F401
+from ._quan_base import (_ActQ, _Conv2dQ, _Conv2dQCiM, _LinearQ, Qmodes, grad_scale,  # noqa: F401
+                         round_pass)
+
+__all__ = ["Conv2dLSQ", "LinearLSQ", "ActLSQ", "Conv2dLSQCiM"]
+
+
+def _act_range(nbits):
+    return 0, 2 ** nbits - 1
+
+
+def _weight_range(nbits):
+    return -(2 ** (nbits - 1)), 2 ** (nbits - 1) - 1
+
+
+def _adc_qp(adcbits):
+    if adcbits in (1, 1.5):
+        return 1
+    return 2 ** (adcbits - 1) - 1
+
+
+class Conv2dLSQCiM(_Conv2dQCiM):
+    """CiM-aware LSQ conv (lsq.py:511-588) on MI355X."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
+                 groups=1, bias=True, nbits_w=8, nbits_a=8, nbits_alpha=8, wbitslice=1, abitslice=1,
+                 xbar=64, adcbits=6, stochastic_quant=False, **kwargs):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
+                         stride=stride, padding=padding, dilation=dilation, groups=groups, bias=bias,
+                         nbits_w=nbits_w, nbits_a=nbits_a, nbits_alpha=nbits_alpha, wbitslice=wbitslice,
+                         abitslice=abitslice, xbar=xbar, adcbits=adcbits, stochastic_quant=stochastic_quant)
+        self._state_cache = None  # host mirror of (init_state, init_state_cim) to avoid a sync per step
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._state_cache = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    def _init_flags(self):
+        if self._state_cache is None:
+            self._state_cache = [bool(self.init_state.item() != 0), bool(self.init_state_cim.item() != 0)]
+        return self._state_cache
+
+    def forward(self, x):
+        qn_w, qp_w = _weight_range(self.nbits_w)
+        qp_adc = _adc_qp(self.adcbits)
+        qn_a, qp_a = _act_range(self.nbits_a)
+        flags = self._init_flags()
+        if self.training and not flags[0]:
+            # lsq.py:532-542: sign detection and LSQ step-size init on the first training step
+            if x.min() < -1e-5:
+                self.signed_act.data.fill_(1)
+            self.alpha_act.data.copy_(2 * x.abs().mean() / math.sqrt(qp_a))
+            self.alpha_weight.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp_w))
+            self.init_state.fill_(1)
+            flags[0] = True
+        if self.binary_mask.device != x.device:
+            self.binary_mask = self.binary_mask.to(x.device)
+        sa = grad_scale(self.alpha_act, 1.0 / math.sqrt(x.numel() * qp_a))            # lsq.py:547-548
+        sw = grad_scale(self.alpha_weight, 1.0 / math.sqrt(self.weight.numel() * qp_w))  # lsq.py:553-554
+        w_q = round_pass((self.weight / sw).clamp(qn_w, qp_w)) * sw                   # lsq.py:555
+        if self.training and not flags[1] and self.alpha_cim is not None:
+            with torch.no_grad():                                                      # lsq.py:557-563
+                a0 = alpha_cim_init(x, w_q, sa, sw, self.binary_mask, self.signed_act, self.stride,
+                                    self.padding, self.nbits_a, self.abitslice, self.nbits_w,
+                                    self.wbitslice, self.adcbits, self.xbar, self.num_xbars)
+                self.alpha_cim.data.copy_(a0)
+                self.init_state_cim.fill_(1)
+            flags[1] = True
+        alpha_q = None
+        if self.alpha_cim is not None:                                                 # lsq.py:566-571
+            qp_al, qn_al = 2 ** self.nbits_alpha - 1, 1
+            a = self.alpha_cim
+            scale = (a.max() - a.min()) / (qp_al - qn_al)
+            alpha_q = round_pass(a / scale).clamp(qn_al, qp_al) * scale
+        if self.adcbits == 0:                                                          # lsq.py:584-585
+            x_q = round_pass((x / sa).clamp(qn_a, qp_a)) * sa
+            return F.conv2d(x_q, w_q, self.bias, self.stride, self.padding, self.dilation)
+        if self.stochastic_quant:
+            raise NotImplementedError("stochastic ADC (lsq.py:205-221) is not implemented on MI355X yet")
+        out = cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, self.binary_mask, self.signed_act, self.stride,
+                             self.padding, self.dilation, self.nbits_a, self.abitslice, self.nbits_w,
+                             self.wbitslice, self.adcbits, self.xbar)
+        fold_x = int((x.shape[-1] - self.weight.shape[-1] + 2 * self.padding[0]) / self.stride[0] + 1)
+        out = out.transpose(1, 2).view(x.shape[0], self.out_channels, fold_x, fold_x)  # lsq.py:580-581
+        if self.bias is not None:
+            out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
+        return out
+
+
+class Conv2dLSQ(_Conv2dQ):
+    """Plain LSQ conv (lsq.py:389-436); consumes the (x_q, act_scale) tuple of ActLSQ."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
+                 groups=1, bias=True, nbits_w=8, **kwargs):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
+                         stride=stride, padding=padding, dilation=dilation, groups=groups, bias=bias,
+                         nbits=nbits_w)
+
+    def forward(self, x):
+        if self.alpha is None:
+            return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        x_q, act_scale = x
+        qn, qp = _weight_range(self.nbits)
+        if self.training and self.init_state == 0:
+            self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
+            self.init_state.fill_(1)
+        ws = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
+        w_q = round_pass((self.weight / ws).clamp(qn, qp))
+        y = F.conv2d(x_q, w_q, self.bias, self.stride, self.padding, self.dilation, self.groups)
+        return y * act_scale * ws
+
+
+class LinearLSQ(_LinearQ):
+    """Plain LSQ linear (lsq.py:591-617)."""
+
+    def __init__(self, in_features, out_features, bias=True, nbits_w=4, **kwargs):
+        super().__init__(in_features=in_features, out_features=out_features, bias=bias, nbits=nbits_w)
+
+    def forward(self, x):
+        if self.alpha is None:
+            return F.linear(x, self.weight, self.bias)
+        qn, qp = _weight_range(self.nbits)
+        if self.training and self.init_state == 0:
+            self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
+            self.init_state.fill_(1)
+        a = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
+        return F.linear(x, round_pass((self.weight / a).clamp(qn, qp)) * a, self.bias)
+
+
+class ActLSQ(_ActQ):
+    """LSQ activation quantiser (lsq.py:620-662): returns (integer codes, step size)."""
+
+    def __init__(self, nbits_a=4, **kwargs):
+        super().__init__(nbits=nbits_a)
+
+    def _range(self):
+        if self.signed == 1:
+            return -(2 ** (self.nbits - 1)), 2 ** (self.nbits - 1) - 1
+        return 0, 2 ** self.nbits - 1
+
+    def forward(self, x):
+        if self.alpha is None:
+            return x
+        if self.training and self.init_state == 0:
+            if x.min() < -1e-5:
+                self.signed.data.fill_(1)
+            _, qp = self._range()
+            self.alpha.data.copy_(2 * x.abs().mean() / math.sqrt(qp))
+            self.init_state.fill_(1)
+        qn, qp = self._range()
+        a = grad_scale(self.alpha, 1.0 / math.sqrt(x.numel() * qp))
+        return round_pass((x / a).clamp(qn, qp)), a

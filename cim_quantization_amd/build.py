@@ -1,0 +1,50 @@
+"""Build libcimq.so in-tree for gfx950 (MI355X) with hipcc.
+
+    python -m cim_quantization_amd.build [--force]
+
+hipcc cross-compiles without a GPU.  ``-ffp-contract=off`` keeps every fp32 operation
+a separate IEEE operation (the bit-exact emulation of the reference's op sequence relies
+on it); fp32 division stays correctly rounded (hipcc's default).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libcimq.so")
+ARCH = os.environ.get("CIMQ_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+                  [os.path.join(REPO, "include", "cimq.h")])
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(s) <= t for s in sources())
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wno-pass-failed",
+           "-o", OUT + ".tmp", os.path.join(CSRC, "cimq_api.hip")]
+    if verbose:
+        print("[cimq] " + " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

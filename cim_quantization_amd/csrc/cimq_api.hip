@@ -1,0 +1,548 @@
+// cimq_api.hip -- the extern "C" boundary of libcimq.so (declared in include/cimq.h).
+// Host-side geometry validation, ctx / workspace carving and the kernel launch sequences
+// that replace get_cim_output_signed.forward / backward (models/_modules/lsq.py:92-386).
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/cimq.h"
+#include "cimq_kernels.hip"
+
+using namespace cimq;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int check_hip(const char* where) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(CIMQ_EHIP, "%s: %s", where, hipGetErrorString(e));
+  return CIMQ_OK;
+}
+
+inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+int make_geo(const cimq_conv_desc* d, Geo* out) {
+  if (!d || !out) return fail(CIMQ_EINVAL, "null descriptor");
+  Geo g;
+  memset(&g, 0, sizeof(g));
+  g.B = d->batch; g.C = d->in_channels; g.H = d->in_h; g.W = d->in_w;
+  g.O = d->out_channels; g.KH = d->kernel_h; g.KW = d->kernel_w;
+  g.SH = d->stride_h; g.SW = d->stride_w; g.PH = d->pad_h; g.PW = d->pad_w;
+  if (g.B <= 0 || g.C <= 0 || g.H <= 0 || g.W <= 0 || g.O <= 0 || g.KH <= 0 || g.KW <= 0 ||
+      g.SH <= 0 || g.SW <= 0 || g.PH < 0 || g.PW < 0)
+    return fail(CIMQ_EINVAL, "bad conv geometry");
+  g.Ho = (g.H + 2 * g.PH - g.KH) / g.SH + 1;
+  g.Wo = (g.W + 2 * g.PW - g.KW) / g.SW + 1;
+  if (g.Ho <= 0 || g.Wo <= 0) return fail(CIMQ_EINVAL, "empty output");
+  g.P = g.Ho * g.Wo;
+  long long M = (long long)g.B * g.P;
+  g.KHW = g.KH * g.KW;
+  g.HW = g.H * g.W;
+  g.K = g.C * g.KHW;
+  long long nin = (long long)g.B * g.C * g.H * g.W;
+  if (M >= (1LL << 31) || nin >= (1LL << 31) || (long long)g.O * g.K >= (1LL << 31))
+    return fail(CIMQ_EUNSUPPORTED, "tensor too large for 32-bit indexing");
+  g.M = (int)M;
+  g.Nin = nin;
+  g.xbar = d->xbar;
+  if (g.xbar <= 0 || g.xbar % 16 != 0 || g.xbar > 128)
+    return fail(CIMQ_EUNSUPPORTED, "xbar must be a positive multiple of 16 and <= 128 (got %d)", g.xbar);
+  g.T = (g.K + g.xbar - 1) / g.xbar;
+  const int tmax = g.K < g.xbar ? g.K : g.xbar;
+  g.KS = (tmax + 63) / 64;
+  g.KTP = g.KS * 64 + 16;
+  g.FBT = (tmax + 15) / 16;
+  if (d->bs_w <= 0 || d->bs_a <= 0 || d->bits_w <= 0 || d->bits_a <= 0)
+    return fail(CIMQ_EINVAL, "bad bit widths");
+  g.bsw = d->bs_w; g.bsa = d->bs_a;
+  g.nbw = d->bits_w / d->bs_w;  // int(bits/bit_slice), lsq.py:115-117
+  g.nba = d->bits_a / d->bs_a;
+  if (g.nbw < 1 || g.nba < 1 || g.nbw > 8 || g.nba > 8)
+    return fail(CIMQ_EUNSUPPORTED, "1..8 bit slices supported (nbw=%d nba=%d)", g.nbw, g.nba);
+  if (g.bsw > 5 || g.bsa > 5) return fail(CIMQ_EUNSUPPORTED, "bit slices wider than 5 bits");
+  if (g.nbw * g.nba > 64) return fail(CIMQ_EUNSUPPORTED, "too many slice pairs");
+  g.NBP = g.nba <= 4 ? 4 : 8;
+  g.Opad = (g.O + 15) / 16 * 16;
+  g.OB16 = g.Opad / 16;
+  g.NBLK = g.nbw * g.OB16;
+  g.NKS = (g.NBLK + 1) / 2;
+  const float ab = d->adc_bits;
+  double qp, qn;
+  if (ab == 0.f) g.mode = ADC_FP;
+  else if (ab == 1.f) g.mode = ADC_SIGN;
+  else if (ab == 1.5f) g.mode = ADC_TERNARY;
+  else if (ab > 1.5f) g.mode = ADC_MULTI;
+  else return fail(CIMQ_EINVAL, "adc_bits %g not one of 0, 1, 1.5 or > 1.5", (double)ab);
+  if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) { qp = 1.0; qn = -1.0; }
+  else { qp = pow(2.0, (double)ab - 1.0) - 1.0; qn = -pow(2.0, (double)ab - 1.0); }  // lsq.py:125-126
+  g.qp = (float)qp; g.qn = (float)qn;
+  g.thr_hi = (float)(qp + 1e-5);  // ps.ge(Qp_adc+1e-5): scalar rounded to fp32
+  g.thr_lo = (float)(qn - 1e-5);
+  g.input_kind = d->input_kind;
+  if (g.input_kind != CIMQ_INPUT_XQ && g.input_kind != CIMQ_INPUT_RAW_LSQ)
+    return fail(CIMQ_EINVAL, "bad input_kind");
+  g.lsq_qp = d->lsq_qp;
+  long long psmax = (long long)tmax * (1LL << g.bsa) * (1LL << g.bsw);
+  g.psmax = (int)(psmax > (1 << 24) ? (1 << 24) : psmax);
+  *out = g;
+  return CIMQ_OK;
+}
+
+struct CtxLayout {
+  size_t xcode, xhat, wfrag, wgx, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, total;
+};
+
+CtxLayout ctx_layout(const Geo& g) {
+  CtxLayout L;
+  size_t o = 0;
+  const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
+  L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);
+  L.xhat = o; o = align256(o + (size_t)g.Nin);
+  L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
+  L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
+  L.thi = o; o = align256(o + npar * 4);
+  L.tlo = o; o = align256(o + npar * 4);
+  L.mlo = o; o = align256(o + npar * 4);
+  L.mhi = o; o = align256(o + npar * 4);
+  L.coef = o; o = align256(o + npar * 4);
+  L.alpha = o; o = align256(o + npar * 4);
+  L.ckj = o; o = align256(o + 3 * 64 * 4);
+  L.flags = o; o = align256(o + 16);
+  L.total = o;
+  return L;
+}
+
+Params params_of(const Geo& g, uint8_t* base) {
+  CtxLayout L = ctx_layout(g);
+  Params p;
+  p.thi = reinterpret_cast<int*>(base + L.thi);
+  p.tlo = reinterpret_cast<int*>(base + L.tlo);
+  p.mlo = reinterpret_cast<int*>(base + L.mlo);
+  p.mhi = reinterpret_cast<int*>(base + L.mhi);
+  p.coef = reinterpret_cast<float*>(base + L.coef);
+  p.alpha = reinterpret_cast<float*>(base + L.alpha);
+  p.ckj = reinterpret_cast<float*>(base + L.ckj);
+  p.flags = reinterpret_cast<int*>(base + L.flags);
+  return p;
+}
+
+// pixel chunking of the gw / init kernel: ~1024 blocks over (chunks x tiles x 32-col groups)
+void gw_chunks(const Geo& g, int* rows_per_chunk, int* nchunks) {
+  const int og = (g.OB16 + 1) / 2;
+  long long want = 1024 / ((long long)g.T * og);
+  if (want < 1) want = 1;
+  long long rows = ((g.M + want - 1) / want + 63) / 64 * 64;
+  if (rows < 64) rows = 64;
+  *rows_per_chunk = (int)rows;
+  *nchunks = cdiv(g.M, rows);
+}
+
+const int kLsqParts = 1024;
+
+size_t lds_tile(const Geo& g) {
+  return align256((size_t)g.nba * 64 * g.KTP + 2 * sizeof(int) * g.KS * 64 + sizeof(int4) * 64);
+}
+size_t lds_gw(const Geo& g) {
+  return lds_tile(g) + sizeof(float) * g.nbw * g.nba * 32 + sizeof(float) * g.FBT * 16 * 32 +
+         (size_t)g.nba * g.KS * 64 * 64;
+}
+const size_t kLdsMax = 160 * 1024;
+
+bool gx_lds_ok(const Geo& g) { return lds_tile(g) + sizeof(float) * g.C * g.HW <= kLdsMax - 1024; }
+
+struct WsLayout {
+  size_t gw_slab, ga_slab, lsq_part, total;
+  int rows, nchunks;
+};
+
+WsLayout ws_layout(const Geo& g) {
+  WsLayout W;
+  gw_chunks(g, &W.rows, &W.nchunks);
+  size_t o = 0;
+  W.gw_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.FBT * 16 * g.Opad);
+  W.ga_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.nbw * g.nba * g.Opad);
+  W.lsq_part = o; o = align256(o + sizeof(float) * kLsqParts);
+  W.total = o;
+  return W;
+}
+
+template <typename K>
+int set_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024) {
+    if (bytes > kLdsMax) return fail(CIMQ_EUNSUPPORTED, "needs %zu bytes of LDS", bytes);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return fail(CIMQ_EHIP, "hipFuncSetAttribute: %s", hipGetErrorString(e));
+  }
+  return CIMQ_OK;
+}
+
+#define CIMQ_TRY(x)        \
+  do {                     \
+    int _rc = (x);         \
+    if (_rc) return _rc;   \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------
+// diagnostic kernel timer (cimq_profile_start / _stop): a hipEvent pair around every launch of
+// one kernel id, recorded on the launch stream; algorithmic bytes / flops per launch follow
+// SURVEY.md section 8(d) (fp32 tensors the kernel must read or write once).
+// ---------------------------------------------------------------------------------------
+enum KernelId { KID_NONE = 0, KID_FWD = 1, KID_BWD_GX = 2, KID_BWD_GW = 3, KID_PREP_ACT = 4 };
+
+struct Profiler {
+  std::mutex mu;
+  int kid = KID_NONE;
+  int cap = 0, n = 0;
+  hipEvent_t* ev = nullptr;  // 2*cap
+  double bytes = 0, flops = 0;
+};
+Profiler& prof() {
+  static Profiler p;
+  return p;
+}
+
+void algo_counts(const Geo& g, int kid, double* bytes, double* flops) {
+  const double x4 = 4.0 * (double)g.Nin, y4 = 4.0 * (double)g.M * g.O;
+  const double mac = (double)g.M * g.O * g.K;
+  switch (kid) {
+    case KID_FWD: *bytes = x4 + y4; *flops = 2.0 * mac; break;             // read x, write y
+    case KID_BWD_GX: *bytes = 2.0 * x4 + y4; *flops = 2.0 * mac * g.nbw; break;  // read gy, x; write gx
+    case KID_BWD_GW: *bytes = x4 + y4; *flops = 2.0 * mac * g.nba; break;  // read gy, x
+    case KID_PREP_ACT: *bytes = x4 + (double)g.Nin * (g.NBP + 1); *flops = 0; break;
+    default: *bytes = 0; *flops = 0;
+  }
+}
+
+// returns the event slot to close after the launch (-1: not profiling this kernel)
+int prof_begin(int kid, const Geo& g, hipStream_t s) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (p.kid != kid || p.n >= p.cap) return -1;
+  const int slot = p.n++;
+  double b, f;
+  algo_counts(g, kid, &b, &f);
+  p.bytes += b;
+  p.flops += f;
+  hipEventRecord(p.ev[2 * slot], s);
+  return slot;
+}
+void prof_end(int slot, hipStream_t s) {
+  if (slot < 0) return;
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> lk(p.mu);
+  hipEventRecord(p.ev[2 * slot + 1], s);
+}
+
+int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, const float* sw,
+             const float* alpha_q, const int8_t* bmask, const float* signed_act, uint8_t* ctx,
+             hipStream_t s, bool need_params, bool need_wgx) {
+  CtxLayout L = ctx_layout(g);
+  const int blk = 256;
+  {
+    int grid = cdiv(g.Nin, blk);
+    if (grid > 8192) grid = 8192;
+    const int slot = prof_begin(KID_PREP_ACT, g, s);
+    hipLaunchKernelGGL(prep_act_kernel, dim3(grid), dim3(blk), 0, s, g, x, sa, signed_act,
+                       reinterpret_cast<int8_t*>(ctx + L.xcode), reinterpret_cast<int8_t*>(ctx + L.xhat));
+    prof_end(slot, s);
+    CIMQ_TRY(check_hip("prep_act"));
+  }
+  {
+    int total = g.T * g.KS * g.NBLK * 64;
+    hipLaunchKernelGGL(prep_wfrag_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
+                       reinterpret_cast<v4i*>(ctx + L.wfrag));
+    CIMQ_TRY(check_hip("prep_wfrag"));
+  }
+  if (need_wgx) {
+    int total = g.T * g.FBT * g.NKS * 64;
+    hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
+                       reinterpret_cast<v4i*>(ctx + L.wgx));
+    CIMQ_TRY(check_hip("prep_wgx"));
+  }
+  Params pp = params_of(g, ctx);
+  if (need_params) {
+    if (hipMemsetAsync(pp.flags, 0, 16, s) != hipSuccess) return fail(CIMQ_EHIP, "memset flags");
+    int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+    hipLaunchKernelGGL(prep_params_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, alpha_q, sw, sa,
+                       bmask, pp);
+    CIMQ_TRY(check_hip("prep_params"));
+  }
+  return CIMQ_OK;
+}
+
+template <int NBP, bool DBG>
+int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
+               float* adc_dbg, hipStream_t s) {
+  CtxLayout L = ctx_layout(g);
+  const size_t lds = lds_tile(g);
+  auto kern = cim_fwd_kernel<NBP, DBG>;
+  CIMQ_TRY(set_lds(kern, lds));
+  dim3 grid(cdiv(g.M, 64), cdiv(g.OB16, 4));
+  const int slot = DBG ? -1 : prof_begin(KID_FWD, g, s);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
+                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ps_dbg,
+                     adc_dbg);
+  prof_end(slot, s);
+  return check_hip("cim_fwd");
+}
+
+template <int NBP, int FBMAX, bool INIT>
+int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
+              const float* gout, uint8_t* ws, hipStream_t s) {
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  const size_t lds = lds_gw(g);
+  auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;
+  CIMQ_TRY(set_lds(kern, lds));
+  dim3 grid(W.nchunks, g.T, (g.OB16 + 1) / 2);
+  const int slot = INIT ? -1 : prof_begin(KID_BWD_GW, g, s);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
+                     reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(ctx + L.wfrag),
+                     params_of(g, const_cast<uint8_t*>(ctx)), sw, sa, signed_act, gout, W.rows,
+                     reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
+  prof_end(slot, s);
+  return check_hip("cim_bwd_gw");
+}
+
+template <int NBP, int FBMAX>
+int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+              float* gx, hipStream_t s) {
+  CtxLayout L = ctx_layout(g);
+  const int8_t* xc = reinterpret_cast<const int8_t*>(ctx + L.xcode);
+  const v4i* wf = reinterpret_cast<const v4i*>(ctx + L.wfrag);
+  const v4i* wg = reinterpret_cast<const v4i*>(ctx + L.wgx);
+  Params pp = params_of(g, const_cast<uint8_t*>(ctx));
+  if (gx_lds_ok(g)) {
+    const size_t lds = lds_tile(g) + sizeof(float) * g.C * g.HW;
+    auto kern = cim_bwd_gx_kernel<NBP, FBMAX, true>;
+    CIMQ_TRY(set_lds(kern, lds));
+    const int slot = prof_begin(KID_BWD_GX, g, s);
+    hipLaunchKernelGGL(kern, dim3(g.B), dim3(256), lds, s, g, xc, wf, wg, pp, sw, sa, gout, gx);
+    prof_end(slot, s);
+    return check_hip("cim_bwd_gx(lds)");
+  }
+  if (hipMemsetAsync(gx, 0, sizeof(float) * g.Nin, s) != hipSuccess) return fail(CIMQ_EHIP, "memset gx");
+  const size_t lds = lds_tile(g);
+  auto kern = cim_bwd_gx_kernel<NBP, FBMAX, false>;
+  CIMQ_TRY(set_lds(kern, lds));
+  const int slot = prof_begin(KID_BWD_GX, g, s);
+  hipLaunchKernelGGL(kern, dim3(cdiv(g.M, 64)), dim3(256), lds, s, g, xc, wf, wg, pp, sw, sa, gout, gx);
+  prof_end(slot, s);
+  CIMQ_TRY(check_hip("cim_bwd_gx(global)"));
+  int grid = cdiv(g.Nin, 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, s, gx, g.Nin, sw, g.nba);
+  return check_hip("scale");
+}
+
+template <int NBP, int FBMAX>
+int launch_bwd_all(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
+                   const float* signed_act, const float* gout, float* gx, uint8_t* ws, hipStream_t s) {
+  CIMQ_TRY((launch_gx<NBP, FBMAX>(g, ctx, sw, sa, gout, gx, s)));
+  CIMQ_TRY((launch_gw<NBP, FBMAX, false>(g, ctx, sw, sa, signed_act, gout, ws, s)));
+  return CIMQ_OK;
+}
+
+template <int NBP>
+int dispatch_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
+                 const float* signed_act, const float* gout, float* gx, uint8_t* ws, hipStream_t s) {
+  if (g.FBT <= 4) return launch_bwd_all<NBP, 4>(g, ctx, sw, sa, signed_act, gout, gx, ws, s);
+  return launch_bwd_all<NBP, 8>(g, ctx, sw, sa, signed_act, gout, gx, ws, s);
+}
+
+template <int NBP>
+int dispatch_init(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
+                  const float* signed_act, uint8_t* ws, hipStream_t s) {
+  if (g.FBT <= 4) return launch_gw<NBP, 4, true>(g, ctx, sw, sa, signed_act, nullptr, ws, s);
+  return launch_gw<NBP, 8, true>(g, ctx, sw, sa, signed_act, nullptr, ws, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cimq_abi_version(void) { return CIMQ_ABI_VERSION; }
+
+const char* cimq_last_error(void) { return g_last_error.c_str(); }
+
+int cimq_query_sizes(const cimq_conv_desc* d, cimq_sizes* out) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!out) return fail(CIMQ_EINVAL, "null output");
+  out->ctx_bytes = ctx_layout(g).total;
+  WsLayout W = ws_layout(g);
+  out->fwd_workspace_bytes = W.total;
+  out->bwd_workspace_bytes = W.total;
+  return CIMQ_OK;
+}
+
+int cimq_forward(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                 const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                 const float* signed_act, float* out, void* ctx, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!x || !w_q || !sa || !sw || !binary_mask || !signed_act || !out || !ctx)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && !alpha_q)
+    return fail(CIMQ_EINVAL, "adc_bits 1 / 1.5 need alpha_q");
+  (void)ws;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
+  CIMQ_TRY(prep_all(g, x, w_q, sa, sw, alpha_q, binary_mask, signed_act, c, s, true, true));
+  if (g.NBP == 4) return launch_fwd<4, false>(g, c, sw, sa, out, nullptr, nullptr, s);
+  return launch_fwd<8, false>(g, c, sw, sa, out, nullptr, nullptr, s);
+}
+
+int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                            const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                            const float* signed_act, float* out, int32_t* ps_out, float* adc_out, void* ctx,
+                            void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!x || !w_q || !sa || !sw || !binary_mask || !signed_act || !out || !ps_out || !adc_out || !ctx)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && !alpha_q)
+    return fail(CIMQ_EINVAL, "adc_bits 1 / 1.5 need alpha_q");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
+  CIMQ_TRY(prep_all(g, x, w_q, sa, sw, alpha_q, binary_mask, signed_act, c, s, true, true));
+  if (g.NBP == 4) return launch_fwd<4, true>(g, c, sw, sa, out, ps_out, adc_out, s);
+  return launch_fwd<8, true>(g, c, sw, sa, out, ps_out, adc_out, s);
+}
+
+int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x, const float* sa,
+                  const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                  const float* signed_act, const void* ctx, float* grad_x, float* grad_w,
+                  float* grad_alpha, float* grad_sa, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  (void)alpha_q; (void)binary_mask;
+  if (!grad_out || !sa || !sw || !signed_act || !ctx || !grad_x || !grad_w || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if (g.input_kind == CIMQ_INPUT_RAW_LSQ && (!x || !grad_sa))
+    return fail(CIMQ_EINVAL, "RAW_LSQ backward needs x and grad_sa");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  if (g.NBP == 4) CIMQ_TRY(dispatch_bwd<4>(g, c, sw, sa, signed_act, grad_out, grad_x, w, s));
+  else CIMQ_TRY(dispatch_bwd<8>(g, c, sw, sa, signed_act, grad_out, grad_x, w, s));
+  WsLayout W = ws_layout(g);
+  hipLaunchKernelGGL(reduce_gw_kernel, dim3(cdiv((long long)g.O * g.K, 256)), dim3(256), 0, s, g, W.nchunks,
+                     reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
+  CIMQ_TRY(check_hip("reduce_gw"));
+  if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && grad_alpha) {
+    const double numel = (double)g.B * g.T * g.nbw * g.nba * g.P * g.O;
+    const float cgrad = (float)(1.0 / sqrt(numel * (double)g.qp));  // lsq.py:323,330
+    hipLaunchKernelGGL(reduce_galpha_kernel, dim3(cdiv((long long)g.T * g.nbw * g.nba * g.O, 256)), dim3(256), 0,
+                       s, g, W.nchunks, reinterpret_cast<const float*>(w + W.ga_slab),
+                       params_of(g, const_cast<uint8_t*>(c)), cgrad, grad_alpha);
+    CIMQ_TRY(check_hip("reduce_galpha"));
+  }
+  if (g.input_kind == CIMQ_INPUT_RAW_LSQ) {
+    int grid = cdiv(g.Nin, 256);
+    if (grid > kLsqParts) grid = kLsqParts;
+    float* part = reinterpret_cast<float*>(w + W.lsq_part);
+    hipLaunchKernelGGL(lsq_act_bwd_kernel, dim3(grid), dim3(256), 0, s, g.Nin, x, sa, g.lsq_qp, grad_x, part);
+    CIMQ_TRY(check_hip("lsq_act_bwd"));
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, grid, part, grad_sa);
+    CIMQ_TRY(check_hip("sum_partials"));
+  }
+  return CIMQ_OK;
+}
+
+int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                    const float* sw, const int8_t* binary_mask, const float* signed_act,
+                    float* alpha_init, void* ctx, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!x || !w_q || !sa || !sw || !binary_mask || !signed_act || !alpha_init || !ctx || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if (!(g.mode == ADC_SIGN || g.mode == ADC_TERNARY))
+    return fail(CIMQ_EINVAL, "alpha_cim exists only for adc_bits 1 / 1.5");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  // the init path slices activations unsigned (lsq.py:51); the fused-LSQ codes are never
+  // negative there, so the signed and unsigned slicings coincide
+  CIMQ_TRY(prep_all(g, x, w_q, sa, sw, nullptr, binary_mask, signed_act, c, s, false, false));
+  {
+    // ckj (mask floats) are not needed by INIT; flags must read 0
+    Params pp = params_of(g, c);
+    if (hipMemsetAsync(pp.flags, 0, 16, s) != hipSuccess) return fail(CIMQ_EHIP, "memset flags");
+  }
+  if (g.NBP == 4) CIMQ_TRY(dispatch_init<4>(g, c, sw, sa, signed_act, w, s));
+  else CIMQ_TRY(dispatch_init<8>(g, c, sw, sa, signed_act, w, s));
+  WsLayout W = ws_layout(g);
+  hipLaunchKernelGGL(reduce_alpha_init_kernel, dim3(cdiv((long long)g.T * g.nbw * g.nba * g.O, 256)), dim3(256), 0,
+                     s, g, W.nchunks, reinterpret_cast<const float*>(w + W.ga_slab), sw, sa,
+                     (float)((double)g.B * g.P), (float)sqrt((double)g.qp), alpha_init);
+  return check_hip("reduce_alpha_init");
+}
+
+int cimq_profile_start(int kernel_id, int max_launches) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (p.ev) return fail(CIMQ_EINVAL, "profiler already running");
+  if (kernel_id < KID_FWD || kernel_id > KID_PREP_ACT || max_launches <= 0)
+    return fail(CIMQ_EINVAL, "bad profiler arguments");
+  p.ev = new hipEvent_t[2 * (size_t)max_launches];
+  for (int i = 0; i < 2 * max_launches; ++i) {
+    if (hipEventCreate(&p.ev[i]) != hipSuccess) {
+      for (int k = 0; k < i; ++k) hipEventDestroy(p.ev[k]);
+      delete[] p.ev;
+      p.ev = nullptr;
+      return fail(CIMQ_EHIP, "hipEventCreate");
+    }
+  }
+  p.kid = kernel_id;
+  p.cap = max_launches;
+  p.n = 0;
+  p.bytes = p.flops = 0;
+  return CIMQ_OK;
+}
+
+int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, double* algo_flops) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (!p.ev) return fail(CIMQ_EINVAL, "profiler not running");
+  double tot = 0;
+  int rc = CIMQ_OK;
+  for (int i = 0; i < p.n; ++i) {
+    float ms = 0;
+    if (hipEventSynchronize(p.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]) != hipSuccess) {
+      rc = fail(CIMQ_EHIP, "hipEventElapsedTime");
+      break;
+    }
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = p.n;
+  if (algo_bytes) *algo_bytes = p.bytes;
+  if (algo_flops) *algo_flops = p.flops;
+  for (int i = 0; i < 2 * p.cap; ++i) hipEventDestroy(p.ev[i]);
+  delete[] p.ev;
+  p.ev = nullptr;
+  p.kid = KID_NONE;
+  p.cap = p.n = 0;
+  return rc;
+}
+
+}  // extern "C"

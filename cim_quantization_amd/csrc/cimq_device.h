@@ -1,0 +1,171 @@
+// cimq_device.h -- geometry, parameter tables and exact-fp32 device helpers shared by the
+// libcimq kernels.  Compiled only for gfx950 (CDNA4): 64-lane waves, MFMA int8/bf16.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace cimq {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+
+enum AdcMode { ADC_FP = 0, ADC_SIGN = 1, ADC_TERNARY = 2, ADC_MULTI = 3 };
+
+// Problem geometry, computed once on the host (cimq_api.hip) and passed by value.
+struct Geo {
+  int B, C, H, W, O, KH, KW, SH, SW, PH, PW, Ho, Wo;
+  int P, M, K, KHW, HW;
+  int xbar, T, KS, KTP;    // KS: 64-deep int8 K-steps per tile, KTP: LDS row pitch (bytes)
+  int FBT;                 // 16-wide f-blocks per tile (ceil(xbar/16))
+  int nbw, nba, bsw, bsa, NBP;  // NBP: bytes per input element in the packed act-code array
+  int Opad, OB16, NBLK, NKS;    // Opad=roundup(O,16); NBLK = nbw*Opad/16; NKS = ceil(NBLK/2)
+  int mode;
+  float qn, qp, thr_hi, thr_lo;  // ADC range; backward clamp thresholds fl32(Qp+1e-5), fl32(Qn-1e-5)
+  int input_kind;
+  float lsq_qp;
+  int psmax;               // bound on |partial sum| used by the threshold search
+  long long Nin;           // B*C*H*W
+};
+
+// Per-(tile i, a-slice j, w-slice k, out-channel o) ADC / STE parameters, SoA.
+// index: ((i*nba + j)*nbw + k)*Opad + o
+struct Params {
+  int* thi;     // forward: ps >= thi -> code +1   (ternary mode)
+  int* tlo;     // forward: ps <= tlo -> code -1
+  int* mlo;     // backward: STE passes iff mlo <= ps <= mhi  (lsq.py:310-313)
+  int* mhi;
+  float* coef;  // alpha_q * binary_mask  (ternary / sign)
+  float* alpha; // alpha_q (literal paths)
+  float* ckj;   // [3][nbw*nba]: mask as float, cE = 2^-(bsa*j)*mask, cD = 2^-(bsw*k)*mask
+  int* flags;   // [0]: literal ADC (degenerate alpha / scales), [1..3] reserved
+};
+
+__host__ __device__ inline int pidx(const Geo& g, int i, int j, int k, int o) {
+  return ((i * g.nba + j) * g.nbw + k) * g.Opad + o;
+}
+
+// ---------------------------------------------------------------------------------------
+// exact fp32 emulation of the reference's torch op sequence (compiled with -ffp-contract=off)
+// ---------------------------------------------------------------------------------------
+__device__ inline float pow2f(int e) { return __int_as_float((127 + e) << 23); }  // |e| < 127
+
+// torch.remainder(t, 2^bs) for float t: floor-mod, result has the divisor's sign.
+__device__ inline float rem_pow2(float t, int bs) {
+  const float b = (float)(1 << bs);
+  return t - b * floorf(t * pow2f(-bs));
+}
+
+// Plane k of the reference's slicing of a non-negative magnitude v (lsq.py:454-457 / 475-478):
+// floor(v / (2^bs)^k) for k >= 1, then remainder 2^bs.
+__device__ inline float slice_mag(float v, int k, int bs) {
+  float t = (k == 0) ? v : floorf(v * pow2f(-bs * k));
+  return rem_pow2(t, bs);
+}
+
+// slicing_act (unsigned, lsq.py:466-480): the same digit extraction on the raw value.
+__device__ inline float slice_unsigned(float v, int k, int bs) { return slice_mag(v, k, bs); }
+
+// slicing_weights_signed / slicing_act_signed (lsq.py:438-464, 483-509): slice the positive
+// part and the negated negative part separately and subtract.
+__device__ inline float slice_signed(float v, int k, int bs) {
+  float pos = (v <= 0.f) ? 0.f : v;
+  float neg = (v >= 0.f) ? 0.f : v;
+  neg = -1.f * neg;
+  return slice_mag(pos, k, bs) - slice_mag(neg, k, bs);
+}
+
+// tensor.type(torch.int8): truncate toward zero, keep the low byte (wraps).  NaN -> 0.
+__device__ inline int to_i8_wrap(float v) {
+  if (!(fabsf(v) < 2147483520.f)) return 0;
+  int t = (int)v;
+  return (int)(int8_t)(t & 0xFF);
+}
+
+__device__ inline int clamp_i8(float v) {
+  v = rintf(v);
+  v = fminf(fmaxf(v, -127.f), 127.f);
+  return (int)v;
+}
+
+// torch.clamp: NaN propagates.
+__device__ inline float clamp_nan(float v, float lo, float hi) {
+  return (v != v) ? v : fminf(fmaxf(v, lo), hi);
+}
+
+// The fp16 store of the partial sums (lsq.py:169,177): an integer ps rounded to half.
+__device__ inline float ps_half(int p) { return __half2float(__float2half_rn((float)p)); }
+
+// u = ps * sw * sa in fp32, in the reference's order (lsq.py:195).
+__device__ inline float u_of(int p, float sw, float sa) {
+  float ps = ps_half(p);
+  float t = ps * sw;
+  return t * sa;
+}
+
+// The ADC of lsq.py:197-230 evaluated literally for one partial sum (no threshold shortcut).
+__device__ inline float adc_literal(int p, int mode, float sw, float sa, float alpha, float qn,
+                                    float qp) {
+  float u = u_of(p, sw, sa);
+  if (mode == ADC_FP) return u;
+  if (mode == ADC_SIGN) {
+    float s = (u > 0.f) ? 1.f : ((u < 0.f) ? -1.f : ((u != u) ? u : 0.f));
+    return s * alpha;
+  }
+  if (mode == ADC_TERNARY) {
+    float v = u / alpha;
+    float q = clamp_nan(rintf(v), qn, qp);
+    return q * alpha;
+  }
+  float d = sw * sa;
+  float v = u / d;
+  float q = clamp_nan(rintf(v), qn, qp);
+  float t = q * sw;
+  return t * sa;
+}
+
+// The backward's rescaled partial sum (lsq.py:257-267).
+__device__ inline float psb_literal(int p, int mode, float sw, float sa, float alpha) {
+  if (mode == ADC_SIGN || mode == ADC_TERNARY) return u_of(p, sw, sa) / alpha;
+  return ps_half(p);
+}
+
+// STE mask (lsq.py:310-313): gradient passes unless clamped.
+__device__ inline bool ste_pass(float psb, float thr_hi, float thr_lo) {
+  return !(psb >= thr_hi || psb <= thr_lo);
+}
+
+// ADC code used by grad_alpha (lsq.py:321-332), literal form.
+__device__ inline float alpha_code_literal(float psb, int mode, float qn, float qp, float thr_hi,
+                                           float thr_lo) {
+  if (mode == ADC_SIGN) return (psb > 0.f) ? 1.f : ((psb < 0.f) ? -1.f : ((psb != psb) ? psb : 0.f));
+  float q = rintf(psb);
+  if (psb >= thr_hi) q = qp;
+  if (psb <= thr_lo) q = qn;
+  return q;
+}
+
+// fp32 -> bf16 round-to-nearest-even (finite inputs) and back
+__device__ inline uint16_t bf16_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  uint32_t r = u + 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(r >> 16);
+}
+__device__ inline float bf16_to_f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Split a float into hi + mid + lo bf16 parts (24 significant bits): the three-term
+// decomposition that gives fp32-accurate products on the bf16 MFMA when the other operand
+// is a small integer (exact in bf16).
+__device__ inline void split3(float a, uint16_t& hi, uint16_t& mid, uint16_t& lo) {
+  hi = bf16_bits(a);
+  float r1 = a - bf16_to_f(hi);
+  mid = bf16_bits(r1);
+  float r2 = r1 - bf16_to_f(mid);
+  lo = bf16_bits(r2);
+}
+
+__device__ inline v8bf as_v8bf(v4i x) { return __builtin_bit_cast(v8bf, x); }
+
+}  // namespace cimq

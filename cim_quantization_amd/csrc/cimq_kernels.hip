@@ -1,0 +1,983 @@
+// cimq_kernels.hip -- CDNA4 (gfx950) kernels for the CiM partial-sum-quantised conv.
+//
+// Data flow (one layer):
+//   prep_act      x (fp32) -> packed per-element act bit-slice codes + int8 ctx code
+//   prep_weight   w_q      -> int8 MFMA fragments of the weight slices (forward / ps
+//                             recompute), bf16 fragments of the truncated slices (grad_x)
+//   prep_params   alpha_q, sw, sa -> integer ADC thresholds + STE intervals per
+//                             (tile, a-slice, w-slice, out-channel)
+//   cim_fwd       implicit im2col -> v_mfma_i32_16x16x64_i8 partial sums -> ADC -> shift-add
+//   cim_bwd_gx    transposed ps recompute -> STE weights E -> bf16x3 MFMA -> col2im in LDS
+//   cim_bwd_gw    ps recompute -> STE weights D, ADC codes -> bf16x3 MFMA over pixels -> slabs
+//   reduce_*      deterministic slab sums (grad_w, grad_alpha, alpha init), LSQ backward
+//
+// Every integer step (codes, slices, partial sums, ADC codes, STE masks) is bit-exact with
+// the reference's fp32 op sequence; the float reductions are fp32 (bf16x3 on MFMA).
+#include "cimq_device.h"
+
+namespace cimq {
+
+#define WAVE 64
+
+// =========================================================================================
+// prep_act: per input element, the forward bit-slice integers and the int8 backward code
+// =========================================================================================
+// x_int = x_q / sa (lsq.py:97); with RAW_LSQ, x_q = round_pass(clamp(x/sa,0,Qp))*sa first
+// (lsq.py:549).  Forward slices follow slicing_act / slicing_act_signed on x_int
+// (lsq.py:146-149) and are stored as rint() int8s (|residue| << 0.5, so the int8 MAC gives
+// round(ps_ref)); ctx code = int8(x_int) (lsq.py:99, truncation + wrap).
+__global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ sa_p,
+                                const float* __restrict__ signed_p, int8_t* __restrict__ xcode,
+                                int8_t* __restrict__ xhat) {
+  const float sa = *sa_p;
+  const bool sgn = (*signed_p) != 0.f;
+  const long long n = g.Nin;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (long long)gridDim.x * blockDim.x) {
+    float v = x[idx];
+    float xq;
+    if (g.input_kind == 1) {
+      float t = v / sa;
+      float c = clamp_nan(t, 0.f, g.lsq_qp);
+      float r = rintf(c);
+      float rp = (r - c) + c;  // round_pass value
+      xq = rp * sa;
+    } else {
+      xq = v;
+    }
+    float xi = xq / sa;
+    xhat[idx] = (int8_t)to_i8_wrap(xi);
+    int8_t out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = 0.f;
+      if (j < g.nba) s = sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa);
+      out[j] = (j < g.nba) ? (int8_t)clamp_i8(s) : (int8_t)0;
+    }
+    if (g.NBP == 4) {
+      uint32_t w = (uint8_t)out[0] | ((uint32_t)(uint8_t)out[1] << 8) |
+                   ((uint32_t)(uint8_t)out[2] << 16) | ((uint32_t)(uint8_t)out[3] << 24);
+      reinterpret_cast<uint32_t*>(xcode)[idx] = w;
+    } else {
+      uint2 w;
+      w.x = (uint8_t)out[0] | ((uint32_t)(uint8_t)out[1] << 8) | ((uint32_t)(uint8_t)out[2] << 16) |
+            ((uint32_t)(uint8_t)out[3] << 24);
+      w.y = (uint8_t)out[4] | ((uint32_t)(uint8_t)out[5] << 8) | ((uint32_t)(uint8_t)out[6] << 16) |
+            ((uint32_t)(uint8_t)out[7] << 24);
+      reinterpret_cast<uint2*>(xcode)[idx] = w;
+    }
+  }
+}
+
+// =========================================================================================
+// prep_weight: MFMA fragments of the weight bit slices
+// =========================================================================================
+// w_int = w_q / sw (lsq.py:98), w_unf = w_int.view(O,-1).t() (lsq.py:153), signed slices
+// (lsq.py:155).  Forward / ps-recompute operand: rint(slice) as int8, stored in the exact
+// per-lane order of v_mfma_i32_16x16x64_i8: wfrag[i][ks][nb][lane][16 bytes], lane l holding
+// rows n = nb*16 + (l&15) (n = k*Opad + o) and contraction f = i*xbar + ks*64 + 16*(l>>4) + e.
+// grad_x operand: int8(slice) (lsq.py:160 truncation) as bf16, wgx[i][fb][s][lane][8]:
+// lane l holds f = i*xbar + fb*16 + (l&15), kappa = (2s + (e>>2))*16 + 4*(l>>4) + (e&3).
+__device__ inline float wslice(const Geo& g, const float* w_q, float sw, int f, int n) {
+  const int k = n / g.Opad, o = n - k * g.Opad;
+  if (f >= g.K || o >= g.O || k >= g.nbw) return 0.f;
+  float wi = w_q[(size_t)o * g.K + f] / sw;
+  return slice_signed(wi, k, g.bsw);
+}
+
+__global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
+                                  v4i* __restrict__ wfrag) {
+  const float sw = *sw_p;
+  const int total = g.T * g.KS * g.NBLK * WAVE;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int lane = t % WAVE;
+    int r = t / WAVE;
+    const int nb = r % g.NBLK;
+    r /= g.NBLK;
+    const int ks = r % g.KS;
+    const int i = r / g.KS;
+    const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+    const int n = nb * 16 + (lane & 15);
+    uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int f = flo + ks * 64 + 16 * (lane >> 4) + e;
+      int v = 0;
+      if (f < fhi) v = clamp_i8(wslice(g, w_q, sw, f, n));
+      wd[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
+    }
+    v4i o;
+    o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
+    wfrag[t] = o;
+  }
+}
+
+__global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
+                                v4i* __restrict__ wgx) {
+  const float sw = *sw_p;
+  const int total = g.T * g.FBT * g.NKS * WAVE;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int lane = t % WAVE;
+    int r = t / WAVE;
+    const int s = r % g.NKS;
+    r /= g.NKS;
+    const int fb = r % g.FBT;
+    const int i = r / g.FBT;
+    const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+    const int f = flo + fb * 16 + (lane & 15);
+    uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kb = 2 * s + (e >> 2);
+      const int kap = kb * 16 + 4 * (lane >> 4) + (e & 3);
+      float v = 0.f;
+      if (f < fhi && kb < g.NBLK) v = (float)to_i8_wrap(wslice(g, w_q, sw, f, kap));
+      const uint32_t h = bf16_bits(v);
+      wd[e >> 1] |= h << (16 * (e & 1));
+    }
+    v4i o;
+    o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
+    wgx[t] = o;
+  }
+}
+
+// =========================================================================================
+// prep_params: ADC thresholds and STE intervals by exact binary search over integer ps
+// =========================================================================================
+// The ADC code and the STE mask are monotone step functions of the integer partial sum
+// (each op in u = fp16(ps)*sw*sa, u/alpha, rint, clamp is monotone for sw*sa > 0 and
+// alpha > 0), so they are captured exactly by integer thresholds found with the very
+// same fp32 ops.  Anything else (alpha_q <= 0 / NaN -- e.g. all-equal alpha_cim gives
+// NaN, lsq.py:570-571 -- or non-positive scales) sets flags[0]: kernels then evaluate
+// the ADC literally per partial sum.
+__device__ inline int first_true_ternary_hi(int lo, int hi, float sw, float sa, float a) {
+  // smallest p in [lo, hi] with rint(u/a) >= 1 ; hi+1 if none
+  int L = lo, R = hi + 1;
+  while (L < R) {
+    int mid = L + ((R - L) >> 1);
+    float q = rintf(u_of(mid, sw, sa) / a);
+    if (q >= 1.f) R = mid; else L = mid + 1;
+  }
+  return L;
+}
+__device__ inline int last_true_ternary_lo(int lo, int hi, float sw, float sa, float a) {
+  // largest p in [lo, hi] with rint(u/a) <= -1 ; lo-1 if none
+  int L = lo - 1, R = hi;
+  while (L < R) {
+    int mid = L + ((R - L + 1) >> 1);
+    float q = rintf(u_of(mid, sw, sa) / a);
+    if (q <= -1.f) L = mid; else R = mid - 1;
+  }
+  return L;
+}
+
+__global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, const float* __restrict__ sw_p,
+                                   const float* __restrict__ sa_p, const int8_t* __restrict__ bmask,
+                                   Params pp) {
+  const float sw = *sw_p, sa = *sa_p;
+  const int npar = g.T * g.nba * g.nbw * g.Opad;
+  const int nkj = g.nbw * g.nba;
+  const bool scales_ok = (sw * sa > 0.f) && isfinite(sw * sa) && isfinite(sw) && isfinite(sa);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < npar + nkj; t += gridDim.x * blockDim.x) {
+    if (t >= npar) {  // per-(k,j) float coefficients
+      const int kj = t - npar, k = kj / g.nba, j = kj - k * g.nba;
+      const float mk = (float)bmask[k * g.nba + j];  // binary_mask[0,0,k,j,0,0]
+      pp.ckj[kj] = mk;
+      pp.ckj[nkj + kj] = mk * pow2f(-g.bsa * j);  // E weight: 2^-(bsa*j) * mask
+      pp.ckj[2 * nkj + kj] = mk * pow2f(-g.bsw * k);  // D weight: 2^-(bsw*k) * mask
+      continue;
+    }
+    int r = t;
+    const int o = r % g.Opad; r /= g.Opad;
+    const int k = r % g.nbw; r /= g.nbw;
+    const int j = r % g.nba;
+    const int i = r / g.nba;
+    const float mk = (float)bmask[k * g.nba + j];
+    float a = 1.f;
+    if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && alpha_q != nullptr && o < g.O)
+      a = alpha_q[((i * g.nbw + k) * g.nba + j) * g.O + o];  // alpha[0,i,k,j,0,o]
+    pp.alpha[t] = a;
+    pp.coef[t] = a * mk;
+    const int lo = -g.psmax - 1, hi = g.psmax + 1;
+    bool literal = false;
+    int thi = hi + 1, tlo = lo - 1, mlo = hi + 1, mhi = lo - 1;
+    if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
+      if (!(scales_ok && a > 0.f && isfinite(a))) literal = true;
+    }
+    if (!literal) {
+      if (g.mode == ADC_TERNARY) {
+        thi = first_true_ternary_hi(lo, hi, sw, sa, a);
+        tlo = last_true_ternary_lo(lo, hi, sw, sa, a);
+      }
+      // STE interval: psb(p) monotone non-decreasing in p
+      {
+        int L = lo, R = hi + 1;  // first p with psb > thr_lo  (i.e. not "<= thr_lo")
+        while (L < R) {
+          int mid = L + ((R - L) >> 1);
+          float b = psb_literal(mid, g.mode, sw, sa, a);
+          if (b > g.thr_lo) R = mid; else L = mid + 1;
+        }
+        mlo = L;
+        L = lo - 1; R = hi;  // last p with psb < thr_hi
+        while (L < R) {
+          int mid = L + ((R - L + 1) >> 1);
+          float b = psb_literal(mid, g.mode, sw, sa, a);
+          if (b < g.thr_hi) L = mid; else R = mid - 1;
+        }
+        mhi = L;
+      }
+    }
+    pp.thi[t] = thi;
+    pp.tlo[t] = tlo;
+    pp.mlo[t] = mlo;
+    pp.mhi[t] = mhi;
+    if (literal) atomicOr(&pp.flags[0], 1);
+  }
+}
+
+// =========================================================================================
+// shared tile machinery: implicit im2col of the packed act codes into LDS
+// =========================================================================================
+// LDS image of one crossbar tile for 64 output pixels: As[j][row][KTP] int8 (row = pixel,
+// contiguous f), built from the packed per-element codes; out-of-image taps are 0 (the
+// zero padding of nn.Unfold).  Tables: foff[f] = c*H*W + kh*W + kw, fkk[f] = kh<<16|kw
+// (-1 = beyond the tile), rowinfo[r] = {img base + ih0*W + iw0, ih0, iw0, valid}.
+struct TileSmem {
+  int8_t* As;     // [nba][64][KTP]
+  int* foff;      // [KS*64]
+  int* fkk;       // [KS*64]
+  int4* rowinfo;  // [64]
+};
+
+__device__ inline void build_rowinfo(const Geo& g, int m0, int4* rowinfo) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int m = m0 + t;
+    int4 ri = make_int4(0, 0, 0, 0);
+    if (m < g.M) {
+      const int b = m / g.P, p = m - b * g.P;
+      const int oh = p / g.Wo, ow = p - oh * g.Wo;
+      const int ih0 = oh * g.SH - g.PH, iw0 = ow * g.SW - g.PW;
+      ri = make_int4(b * g.C * g.HW + ih0 * g.W + iw0, ih0, iw0, 1);
+    }
+    rowinfo[t] = ri;
+  }
+}
+
+__device__ inline void build_ftable(const Geo& g, int i, int* foff, int* fkk) {
+  const int flo = i * g.xbar, flen = min(g.xbar, g.K - flo);
+  for (int t = threadIdx.x; t < g.KS * 64; t += blockDim.x) {
+    if (t < flen) {
+      const int f = flo + t;
+      const int c = f / g.KHW, rem = f - c * g.KHW;
+      const int kh = rem / g.KW, kw = rem - kh * g.KW;
+      foff[t] = c * g.HW + kh * g.W + kw;
+      fkk[t] = (kh << 16) | kw;
+    } else {
+      foff[t] = 0;
+      fkk[t] = -1;
+    }
+  }
+}
+
+// Gather one element's packed code (all slices) for pixel row r and tile column t.
+template <int NBP>
+__device__ inline uint2 gather_code(const Geo& g, const int8_t* __restrict__ xcode, const int4 ri,
+                                    int fo, int fk) {
+  uint2 c = make_uint2(0, 0);
+  if (fk >= 0 && ri.w) {
+    const int kh = fk >> 16, kw = fk & 0xFFFF;
+    const int ih = ri.y + kh, iw = ri.z + kw;
+    if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+      const long long idx = (long long)ri.x + fo;
+      if (NBP == 4) c.x = reinterpret_cast<const uint32_t*>(xcode)[idx];
+      else c = reinterpret_cast<const uint2*>(xcode)[idx];
+    }
+  }
+  return c;
+}
+
+// Build As for the 64 pixels of rowinfo and tile (foff/fkk): each work item is 4
+// consecutive tile columns of one pixel; the per-slice bytes are transposed into one
+// dword per slice plane.
+template <int NBP>
+__device__ inline void build_As(const Geo& g, const int8_t* __restrict__ xcode, const TileSmem& sm) {
+  const int quads = g.KS * 16;
+  const int items = 64 * quads;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int r = it / quads, q = it - r * quads;
+    const int4 ri = sm.rowinfo[r];
+    uint32_t pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int t = 4 * q + e;
+      const uint2 c = gather_code<NBP>(g, xcode, ri, sm.foff[t], sm.fkk[t]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pl[j] |= ((c.x >> (8 * j)) & 0xFFu) << (8 * e);
+      if (NBP == 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pl[4 + j] |= ((c.y >> (8 * j)) & 0xFFu) << (8 * e);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < g.nba) *reinterpret_cast<uint32_t*>(sm.As + ((size_t)j * 64 + r) * g.KTP + 4 * q) = pl[j];
+  }
+}
+
+// Load the 16-byte MFMA operand of slice plane j for row (base16 + (lane&15)).
+__device__ inline v4i load_xfrag(const Geo& g, const int8_t* As, int j, int row, int ks, int lane) {
+  const int8_t* p = As + ((size_t)j * 64 + row) * g.KTP + ks * 64 + 16 * (lane >> 4);
+  return *reinterpret_cast<const v4i*>(p);
+}
+
+// =========================================================================================
+// cim_fwd: partial sums + ADC + shift-and-add   (lsq.py:166-233)
+// =========================================================================================
+// Block = 64 output pixels x one 64-column output-channel group; wave w owns pixels
+// [16w, 16w+16).  For every tile i, a-slice j, w-slice k:  ps = X_j(16 x tile) . W_k(tile x 16)
+// on v_mfma_i32_16x16x64_i8 (exact integers), then the ADC code and out += code*alpha*mask.
+// DBG: additionally write every integer partial sum and its ADC output (before the
+// shift-and-add mask) in the reference's [B, T, nbw, nba, P, O] order (the ctx.ps_int of
+// lsq.py:192 and adc_out of lsq.py:197-230) -- the parity hook of cimq_debug_partial_sums.
+template <int NBP, bool DBG>
+__global__ __launch_bounds__(256) void cim_fwd_kernel(Geo g, const int8_t* __restrict__ xcode,
+                                                      const v4i* __restrict__ wfrag, Params pp,
+                                                      const float* __restrict__ sw_p,
+                                                      const float* __restrict__ sa_p,
+                                                      float* __restrict__ out, int* __restrict__ ps_dbg,
+                                                      float* __restrict__ adc_dbg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  TileSmem sm;
+  sm.As = reinterpret_cast<int8_t*>(smem);
+  size_t off = (size_t)g.nba * 64 * g.KTP;
+  sm.foff = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.fkk = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.rowinfo = reinterpret_cast<int4*>(smem + off);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int m0 = blockIdx.x * 64;
+  const int og = blockIdx.y;
+  const int nob = min(4, g.OB16 - og * 4);
+  const float sw = *sw_p, sa = *sa_p;
+  const bool literal = (pp.flags[0] != 0) || g.mode != ADC_TERNARY;
+  const int nkj = g.nbw * g.nba;
+
+  build_rowinfo(g, m0, sm.rowinfo);
+  float acc_out[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc_out[a][b] = 0.f;
+
+  for (int i = 0; i < g.T; ++i) {
+    __syncthreads();
+    build_ftable(g, i, sm.foff, sm.fkk);
+    __syncthreads();
+    build_As<NBP>(g, xcode, sm);
+    __syncthreads();
+    for (int j = 0; j < g.nba; ++j) {
+      v4i a[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        if (ks < g.KS) a[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
+      for (int k = 0; k < g.nbw; ++k) {
+        const float mk = pp.ckj[k * g.nba + j];
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          if (ob < nob) {
+            const int nb = k * g.OB16 + og * 4 + ob;
+            v4i acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+              if (ks < g.KS)
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                    a[ks], wfrag[((size_t)(i * g.KS + ks) * g.NBLK + nb) * WAVE + lane], acc, 0, 0, 0);
+            const int o = (og * 4 + ob) * 16 + r16;
+            const int pi = pidx(g, i, j, k, o);
+            if (DBG) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wave * 16 + 4 * g4 + r;
+                if (m < g.M && o < g.O) {
+                  const int b = m / g.P, p = m - b * g.P;
+                  const size_t di = ((((size_t)b * g.T + i) * g.nbw + k) * g.nba + j) * g.P * g.O +
+                                    (size_t)p * g.O + o;
+                  ps_dbg[di] = acc[r];
+                  float adc;
+                  if (!literal) {
+                    const float q = (acc[r] >= pp.thi[pi]) ? 1.f : ((acc[r] <= pp.tlo[pi]) ? -1.f : 0.f);
+                    adc = q * pp.alpha[pi];
+                  } else {
+                    adc = adc_literal(acc[r], g.mode, sw, sa, pp.alpha[pi], g.qn, g.qp);
+                  }
+                  adc_dbg[di] = adc;
+                }
+              }
+            }
+            if (!literal) {
+              const int thi = pp.thi[pi], tlo = pp.tlo[pi];
+              const float cf = pp.coef[pi];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int ps = acc[r];
+                float v = (ps >= thi) ? cf : 0.f;
+                v -= (ps <= tlo) ? cf : 0.f;
+                acc_out[ob][r] += v;
+              }
+            } else {
+              const float al = pp.alpha[pi];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float adc = adc_literal(acc[r], g.mode, sw, sa, al, g.qn, g.qp);
+                acc_out[ob][r] += adc * mk;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  (void)nkj;
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    if (ob < nob) {
+      const int o = (og * 4 + ob) * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wave * 16 + 4 * g4 + r;
+        if (m < g.M && o < g.O) out[(size_t)m * g.O + o] = acc_out[ob][r];
+      }
+    }
+  }
+}
+
+// =========================================================================================
+// cim_bwd_gx: grad wrt the activation   (lsq.py:338-382, closed form)
+// =========================================================================================
+//   gx_unf[m,f] = (sw/nba) * sum_{k,o} g[m,o] * E_k[m,i(f),o] * w^_k[f,o]
+//   E_k = sum_j 2^-(bsa*j) * mask[k,j] * STE[m,i,k,j,o]
+// ps is recomputed TRANSPOSED (rows kappa=(k,o), columns = pixels) so each accumulator is
+// directly the B operand of the next bf16 MFMA (contraction over kappa, no LDS transpose);
+// g*E is split into three bf16 terms.  The im2col adjoint (nn.Fold) is an LDS scatter-add
+// into the block's image (LDS_ACC) or, for images too large for LDS, global atomics.
+template <int NBP, int FBMAX, bool LDS_ACC>
+__global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __restrict__ xcode,
+                                                         const v4i* __restrict__ wfrag,
+                                                         const v4i* __restrict__ wgx, Params pp,
+                                                         const float* __restrict__ sw_p,
+                                                         const float* __restrict__ sa_p,
+                                                         const float* __restrict__ gout,
+                                                         float* __restrict__ gx) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  TileSmem sm;
+  sm.As = reinterpret_cast<int8_t*>(smem);
+  size_t off = (size_t)g.nba * 64 * g.KTP;
+  sm.foff = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.fkk = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.rowinfo = reinterpret_cast<int4*>(smem + off); off += sizeof(int4) * 64;
+  float* gxacc = reinterpret_cast<float*>(smem + off);  // [C*H*W] when LDS_ACC
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sw = *sw_p, sa = *sa_p;
+  const bool literal = (pp.flags[0] != 0);
+  const int nkj = g.nbw * g.nba;
+  const int chw = g.C * g.HW;
+
+  int mbeg, mend;
+  if (LDS_ACC) {
+    const int b = blockIdx.x;
+    mbeg = b * g.P;
+    mend = mbeg + g.P;
+    for (int t = threadIdx.x; t < chw; t += blockDim.x) gxacc[t] = 0.f;
+  } else {
+    mbeg = blockIdx.x * 64;
+    mend = min(mbeg + 64, g.M);
+  }
+
+  for (int m0 = mbeg; m0 < mend; m0 += 64) {
+    __syncthreads();
+    build_rowinfo(g, m0, sm.rowinfo);
+    if (LDS_ACC && threadIdx.x < 64 && m0 + (int)threadIdx.x >= mend) sm.rowinfo[threadIdx.x].w = 0;
+    for (int i = 0; i < g.T; ++i) {
+      __syncthreads();
+      build_ftable(g, i, sm.foff, sm.fkk);
+      __syncthreads();
+      build_As<NBP>(g, xcode, sm);
+      __syncthreads();
+
+      const int mcol = m0 + wave * 16 + r16;  // this lane's pixel (accumulator column)
+      const bool mvalid = sm.rowinfo[wave * 16 + r16].w != 0;
+      v4f gxa[FBMAX];
+#pragma unroll
+      for (int fb = 0; fb < FBMAX; ++fb) gxa[fb] = v4f{0.f, 0.f, 0.f, 0.f};
+
+      for (int kc = 0; kc < g.NBLK; kc += 8) {  // chunk of 8 kappa-blocks (4 MFMA K-steps)
+        float E[8][4];
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) E[a][b] = 0.f;
+        for (int j = 0; j < g.nba; ++j) {
+          v4i xb[4];
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+            if (ks < g.KS) xb[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const int kb = kc + kk;
+            if (kb < g.NBLK) {
+              v4i acc = {0, 0, 0, 0};
+#pragma unroll
+              for (int ks = 0; ks < 4; ++ks)
+                if (ks < g.KS)
+                  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                      wfrag[((size_t)(i * g.KS + ks) * g.NBLK + kb) * WAVE + lane], xb[ks], acc, 0, 0, 0);
+              const int k = kb / g.OB16;
+              const int obase = (kb - k * g.OB16) * 16 + 4 * g4;
+              const float ce = pp.ckj[nkj + k * g.nba + j];
+              const int pi = pidx(g, i, j, k, obase);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                bool pass;
+                if (!literal) {
+                  pass = (acc[r] >= pp.mlo[pi + r]) && (acc[r] <= pp.mhi[pi + r]);
+                } else {
+                  const float b = psb_literal(acc[r], g.mode, sw, sa, pp.alpha[pi + r]);
+                  pass = ste_pass(b, g.thr_hi, g.thr_lo);
+                }
+                E[kk][r] += pass ? ce : 0.f;
+              }
+            }
+          }
+        }
+        // B operands: (g * E)[kappa, pixel], kappa-step s covers kappa-blocks kc+2s, kc+2s+1
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kb0 = kc + 2 * s;
+          if (kb0 < g.NBLK) {
+            uint32_t hi[4] = {0, 0, 0, 0}, mi[4] = {0, 0, 0, 0}, lo[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int kb = kb0 + (e >> 2);
+              const int r = e & 3;
+              float av = 0.f;
+              if (kb < g.NBLK && mvalid) {
+                const int k = kb / g.OB16;
+                const int o = (kb - k * g.OB16) * 16 + 4 * g4 + r;
+                if (o < g.O) av = gout[(size_t)mcol * g.O + o] * E[2 * s + (e >> 2)][r];
+              }
+              uint16_t h, md, l;
+              split3(av, h, md, l);
+              hi[e >> 1] |= (uint32_t)h << (16 * (e & 1));
+              mi[e >> 1] |= (uint32_t)md << (16 * (e & 1));
+              lo[e >> 1] |= (uint32_t)l << (16 * (e & 1));
+            }
+            const v8bf bh = as_v8bf(v4i{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]});
+            const v8bf bm = as_v8bf(v4i{(int)mi[0], (int)mi[1], (int)mi[2], (int)mi[3]});
+            const v8bf bl = as_v8bf(v4i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]});
+            const int sg = kc / 2 + s;
+#pragma unroll
+            for (int fb = 0; fb < FBMAX; ++fb) {
+              if (fb < g.FBT) {
+                const v8bf wa = as_v8bf(wgx[((size_t)(i * g.FBT + fb) * g.NKS + sg) * WAVE + lane]);
+                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bh, gxa[fb], 0, 0, 0);
+                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bm, gxa[fb], 0, 0, 0);
+                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bl, gxa[fb], 0, 0, 0);
+              }
+            }
+          }
+        }
+      }
+      // scatter gx_unf[f, pixel] -> image (col2im / nn.Fold adjoint of the unfold)
+      if (mvalid) {
+        const int4 ri = sm.rowinfo[wave * 16 + r16];
+#pragma unroll
+        for (int fb = 0; fb < FBMAX; ++fb) {
+          if (fb < g.FBT) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int t = fb * 16 + 4 * g4 + r;
+              const int fk = (t < g.KS * 64) ? sm.fkk[t] : -1;
+              if (fk >= 0) {
+                const int ih = ri.y + (fk >> 16), iw = ri.z + (fk & 0xFFFF);
+                if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
+                  const float v = gxa[fb][r];
+                  if (LDS_ACC) {
+                    const int b = mcol / g.P;
+                    atomicAdd(&gxacc[ri.x - b * chw + sm.foff[t]], v);
+                  } else {
+                    atomicAdd(&gx[(size_t)ri.x + sm.foff[t]], v);
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  if (LDS_ACC) {
+    __syncthreads();
+    const float scale = sw / (float)g.nba;
+    const size_t base = (size_t)blockIdx.x * chw;
+    for (int t = threadIdx.x; t < chw; t += blockDim.x) gx[base + t] = gxacc[t] * scale;
+  }
+}
+
+__global__ void scale_kernel(float* __restrict__ v, long long n, const float* __restrict__ sw_p, int nba) {
+  const float scale = (*sw_p) / (float)nba;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    v[i] *= scale;
+}
+
+// =========================================================================================
+// cim_bwd_gw: grad wrt the weights and alpha_cim; alpha_cim init   (lsq.py:321-369, 35-87)
+// =========================================================================================
+//   gw[f,o] = (sa/nbw) * sum_j sum_m xhat_j[m,f] * g[m,o] * D_j[m,i(f),o]
+//   D_j = sum_k 2^-(bsw*k) * mask[k,j] * STE[m,i,k,j,o]
+//   galpha[i,k,j,o] = c * mask[k,j] * sum_m code[m,i,k,j,o] * g[m,o]
+// Block = (tile i, 32-channel group, pixel chunk).  ps is recomputed in the natural
+// orientation (rows = pixels), so g*D is directly the B operand of a bf16 MFMA that
+// contracts over (pixel, a-slice) against the int8 ctx slices xhat_j (lsq.py:290-295).
+// INIT mode accumulates sum_m |ps*sw*sa| instead (fp32 partial sums of lsq.py:64).
+template <int NBP, int FBMAX, bool INIT>
+__global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __restrict__ xcode,
+                                                         const int8_t* __restrict__ xhat,
+                                                         const v4i* __restrict__ wfrag, Params pp,
+                                                         const float* __restrict__ sw_p,
+                                                         const float* __restrict__ sa_p,
+                                                         const float* __restrict__ signed_p,
+                                                         const float* __restrict__ gout, int rows_per_chunk,
+                                                         float* __restrict__ gw_slab,
+                                                         float* __restrict__ ga_slab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  TileSmem sm;
+  sm.As = reinterpret_cast<int8_t*>(smem);
+  size_t off = (size_t)g.nba * 64 * g.KTP;
+  sm.foff = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.fkk = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
+  sm.rowinfo = reinterpret_cast<int4*>(smem + off); off += sizeof(int4) * 64;
+  const int tlen = g.KS * 64;
+  const int nkj = g.nbw * g.nba;
+  const int ncol = 32;
+  float* qacc = reinterpret_cast<float*>(smem + off);   // [nkj][32]: sum code*g (|u| in INIT)
+  off += sizeof(float) * nkj * ncol;
+  float* gwacc = reinterpret_cast<float*>(smem + off);  // [FBT*16][32]
+  off += sizeof(float) * g.FBT * 16 * ncol;
+  int8_t* Xb = reinterpret_cast<int8_t*>(smem + off);   // [nba][tlen][64] bwd slices, f-major
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int i = blockIdx.y;
+  const int og = blockIdx.z;  // 32-channel group: o-blocks 2*og, 2*og+1
+  const int nob = min(2, g.OB16 - og * 2);
+  const int mc = blockIdx.x;
+  const int mbeg = mc * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
+  const float sw = *sw_p, sa = *sa_p;
+  const bool sgn = (*signed_p) != 0.f;
+  const bool literal = (pp.flags[0] != 0);
+  const bool ternary_fast = (!literal) && g.mode == ADC_TERNARY;
+  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
+
+  for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) qacc[t] = 0.f;
+  for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
+  v4f gwa[FBMAX][2];
+#pragma unroll
+  for (int a = 0; a < FBMAX; ++a) { gwa[a][0] = v4f{0, 0, 0, 0}; gwa[a][1] = v4f{0, 0, 0, 0}; }
+
+  build_ftable(g, i, sm.foff, sm.fkk);
+  for (int m0 = mbeg; m0 < mend; m0 += 64) {
+    __syncthreads();
+    build_rowinfo(g, m0, sm.rowinfo);
+    if (threadIdx.x < 64 && m0 + (int)threadIdx.x >= mend) sm.rowinfo[threadIdx.x].w = 0;
+    __syncthreads();
+    build_As<NBP>(g, xcode, sm);
+    if (!INIT) {
+      // backward act slices of the int8 ctx code (lsq.py:290-295), f-major: Xb[j][t][row]
+      for (int it = threadIdx.x; it < tlen * 16; it += blockDim.x) {
+        const int t = it >> 4, rq = (it & 15) * 4;
+        const int fk = sm.fkk[t];
+        uint32_t pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int4 ri = sm.rowinfo[rq + e];
+          float xv = 0.f;
+          if (fk >= 0 && ri.w) {
+            const int ih = ri.y + (fk >> 16), iw = ri.z + (fk & 0xFFFF);
+            if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) xv = (float)xhat[(size_t)ri.x + sm.foff[t]];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (j < g.nba) {
+              const float s = sgn ? slice_signed(xv, j, g.bsa) : slice_unsigned(xv, j, g.bsa);
+              pl[j] |= ((uint32_t)(uint8_t)(int8_t)clamp_i8(s)) << (8 * e);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < g.nba) *reinterpret_cast<uint32_t*>(Xb + ((size_t)j * tlen + t) * 64 + rq) = pl[j];
+      }
+    }
+    __syncthreads();
+
+    const int rowbase = wave * 16 + 4 * g4;  // this lane's 4 accumulator rows (pixels)
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) {
+      if (ob < nob) {
+        const int ocol = ob * 16 + r16;
+        const int o = og * 32 + ocol;
+        float gval[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + rowbase + r;
+          gval[r] = (!INIT && o < g.O && sm.rowinfo[rowbase + r].w) ? gout[(size_t)m * g.O + o] : 0.f;
+        }
+        float D[8][4];
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) D[a][b] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j < g.nba) {
+            v4i xa[4];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+              if (ks < g.KS) xa[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
+            for (int k = 0; k < g.nbw; ++k) {
+              const int nb = k * g.OB16 + og * 2 + ob;
+              v4i acc = {0, 0, 0, 0};
+#pragma unroll
+              for (int ks = 0; ks < 4; ++ks)
+                if (ks < g.KS)
+                  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                      xa[ks], wfrag[((size_t)(i * g.KS + ks) * g.NBLK + nb) * WAVE + lane], acc, 0, 0, 0);
+              const int pi = pidx(g, i, j, k, o);
+              const int kj = k * g.nba + j;
+              float qs = 0.f;
+              if (INIT) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float u = ((float)acc[r] * sw) * sa;  // fp32 ps (no fp16 store), lsq.py:64,84
+                  qs += fabsf(u);
+                }
+              } else {
+                const float cd = pp.ckj[2 * nkj + kj];
+                if (ternary_fast) {
+                  const int mlo = pp.mlo[pi], mhi = pp.mhi[pi], thi = pp.thi[pi], tlo = pp.tlo[pi];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    const int p = acc[r];
+                    D[j][r] += ((p >= mlo) && (p <= mhi)) ? cd : 0.f;
+                    const float q = (p >= thi) ? 1.f : ((p <= tlo) ? -1.f : 0.f);
+                    qs += q * gval[r];
+                  }
+                } else {
+                  const float al = pp.alpha[pi];
+                  const int mlo = pp.mlo[pi], mhi = pp.mhi[pi];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    const int p = acc[r];
+                    const float b = psb_literal(p, g.mode, sw, sa, al);
+                    const bool pass = literal ? ste_pass(b, g.thr_hi, g.thr_lo) : ((p >= mlo) && (p <= mhi));
+                    D[j][r] += pass ? cd : 0.f;
+                    if (has_code) qs += alpha_code_literal(b, g.mode, g.qn, g.qp, g.thr_hi, g.thr_lo) * gval[r];
+                  }
+                }
+              }
+              // lanes l, l^16, l^32, l^48 share the column: fold the 16 pixel rows, then LDS
+              qs += __shfl_xor(qs, 16);
+              qs += __shfl_xor(qs, 32);
+              if (g4 == 0 && (INIT || has_code)) atomicAdd(&qacc[kj * ncol + ocol], qs);
+            }
+          }
+        }
+        if (!INIT) {
+          // gw MFMA: contraction over kappa = (pixel row r of this lane's 4, a-slice j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            if (2 * s < g.nba) {
+              uint32_t hi[4] = {0, 0, 0, 0}, mi[4] = {0, 0, 0, 0}, lo[4] = {0, 0, 0, 0};
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const int j = 2 * s + (e >> 2), r = e & 3;
+                const float bv = (j < g.nba) ? gval[r] * D[j][r] : 0.f;
+                uint16_t h, md, l;
+                split3(bv, h, md, l);
+                hi[e >> 1] |= (uint32_t)h << (16 * (e & 1));
+                mi[e >> 1] |= (uint32_t)md << (16 * (e & 1));
+                lo[e >> 1] |= (uint32_t)l << (16 * (e & 1));
+              }
+              const v8bf bh = as_v8bf(v4i{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]});
+              const v8bf bm = as_v8bf(v4i{(int)mi[0], (int)mi[1], (int)mi[2], (int)mi[3]});
+              const v8bf bl = as_v8bf(v4i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]});
+#pragma unroll
+              for (int fb = 0; fb < FBMAX; ++fb) {
+                if (fb < g.FBT) {
+                  const int t = fb * 16 + r16;
+                  uint32_t ad[4] = {0, 0, 0, 0};
+#pragma unroll
+                  for (int h2 = 0; h2 < 2; ++h2) {
+                    const int j = 2 * s + h2;
+                    uint32_t bytes = 0;
+                    if (j < g.nba)
+                      bytes = *reinterpret_cast<const uint32_t*>(Xb + ((size_t)j * tlen + t) * 64 + rowbase);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                      const float xv = (float)(int8_t)((bytes >> (8 * r)) & 0xFF);
+                      const int e = h2 * 4 + r;
+                      ad[e >> 1] |= (uint32_t)bf16_bits(xv) << (16 * (e & 1));
+                    }
+                  }
+                  const v8bf xa8 = as_v8bf(v4i{(int)ad[0], (int)ad[1], (int)ad[2], (int)ad[3]});
+                  v4f accw = gwa[fb][ob];
+                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa8, bh, accw, 0, 0, 0);
+                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa8, bm, accw, 0, 0, 0);
+                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa8, bl, accw, 0, 0, 0);
+                  gwa[fb][ob] = accw;
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---- block reductions -> slabs (deterministic across blocks; in-block LDS order) ----
+  if (!INIT) {
+#pragma unroll
+    for (int fb = 0; fb < FBMAX; ++fb)
+      if (fb < g.FBT)
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+          if (ob < nob)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * ncol + ob * 16 + r16], gwa[fb][ob][r]);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) {
+    const int q = t / ncol, col = t - q * ncol;
+    const int o = og * 32 + col;
+    if (o < g.Opad) {
+      const int k = q / g.nba, j = q - k * g.nba;
+      ga_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qacc[t];
+    }
+  }
+  if (INIT) return;
+  for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) {
+    const int fl = t / ncol, col = t - fl * ncol;
+    const int o = og * 32 + col;
+    if (o < g.Opad) gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o] = gwacc[t];
+  }
+}
+
+
+// grad_w[o, f] = (sa/nbw) * sum_chunks slab ;  grad_alpha = c * mask * sum_chunks
+__global__ void reduce_gw_kernel(Geo g, int nchunks, const float* __restrict__ gw_slab,
+                                 const float* __restrict__ sa_p, float* __restrict__ grad_w) {
+  const float scale = (*sa_p) / (float)g.nbw;
+  const int total = g.O * g.K;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int o = t / g.K, f = t - o * g.K;
+    const int i = f / g.xbar, fl = f - i * g.xbar;
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c) s += gw_slab[(((size_t)c * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o];
+    grad_w[t] = s * scale;
+  }
+}
+
+__global__ void reduce_galpha_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab, Params pp,
+                                     float cgrad, float* __restrict__ grad_alpha) {
+  const int nkj = g.nbw * g.nba;
+  const int total = g.T * nkj * g.O;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    // output layout [1, T, nbw, nba, 1, O]
+    int r = t;
+    const int o = r % g.O; r /= g.O;
+    const int j = r % g.nba; r /= g.nba;
+    const int k = r % g.nbw;
+    const int i = r / g.nbw;
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c)
+      s += ga_slab[(((size_t)c * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o];
+    grad_alpha[t] = (cgrad * pp.ckj[k * g.nba + j]) * s;
+  }
+}
+
+// alpha_init = 2*mean|u|/sqrt(Qp_adc); zeros -> sw*sa   (lsq.py:560-562)
+__global__ void reduce_alpha_init_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab,
+                                         const float* __restrict__ sw_p, const float* __restrict__ sa_p,
+                                         float count, float sqrt_qp, float* __restrict__ alpha_init) {
+  const int nkj = g.nbw * g.nba;
+  const int total = g.T * nkj * g.O;
+  const float fill = (1.0f * (*sw_p)) * (*sa_p);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    int r = t;
+    const int o = r % g.O; r /= g.O;
+    const int j = r % g.nba; r /= g.nba;
+    const int k = r % g.nbw;
+    const int i = r / g.nbw;
+    float s = 0.f;
+    for (int c = 0; c < nchunks; ++c)
+      s += ga_slab[(((size_t)c * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o];
+    const float mean = s / count;
+    float v = (2.0f * mean) / sqrt_qp;
+    alpha_init[t] = (v == 0.f) ? fill : v;
+  }
+}
+
+// =========================================================================================
+// LSQ activation quantiser backward (autograd of lsq.py:547-549, fused-module path)
+// =========================================================================================
+//   y1 = x/sa ; c = clamp(y1,0,Qp) ; x_q = round_pass(c)*sa
+//   g_y1 = (0<=y1<=Qp) ? g*sa : 0 ;  g_x = g_y1/sa
+//   g_sa = sum(g*round(c)) + sum(-g_y1*((x/sa)/sa))
+__global__ void lsq_act_bwd_kernel(long long n, const float* __restrict__ x, const float* __restrict__ sa_p,
+                                   float qp, float* __restrict__ gx_inout, float* __restrict__ partial) {
+  __shared__ float sred[256];
+  const float sa = *sa_p;
+  float acc = 0.f;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const float xv = x[idx];
+    const float gq = gx_inout[idx];
+    const float y1 = xv / sa;
+    const float c = clamp_nan(y1, 0.f, qp);
+    const float r = rintf(c);
+    const float rp = (r - c) + c;
+    const bool pass = (y1 >= 0.f) && (y1 <= qp);
+    const float gy = pass ? gq * sa : 0.f;
+    gx_inout[idx] = gy / sa;
+    acc += gq * rp;
+    acc += -(gy * (y1 / sa));
+  }
+  sred[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sred[threadIdx.x] += sred[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sred[0];
+}
+
+__global__ void sum_partials_kernel(int n, const float* __restrict__ partial, float* __restrict__ out) {
+  __shared__ float sred[256];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += partial[i];
+  sred[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sred[threadIdx.x] += sred[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sred[0];
+}
+
+}  // namespace cimq

@@ -1,0 +1,235 @@
+"""Autograd Functions backed by libcimq (HIP, gfx950).
+
+``get_cim_output_signed``  drop-in for the reference Function of the same name
+                           (models/_modules/lsq.py:89-386): same 17 positional args,
+                           same [B, P, O] output, same 17-tuple of grads.
+``cim_conv2d_lsq``         the fused path used by ``Conv2dLSQCiM``: the activation LSQ
+                           quantiser (lsq.py:547-549) runs inside the CiM kernels, so x_q
+                           is never materialised; grads flow to x and to the step size sa.
+
+Device-only: CPU tensors raise (there is no CPU fallback in the product path).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("cim_quantization_amd runs on ROCm devices only (got a CPU tensor); "
+                               "the CPU restatement lives in oracle/ and is test infrastructure")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _f32(t, device):
+    t = t if torch.is_tensor(t) else torch.tensor(t)
+    return t.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
+def _geometry(x, w, stride, padding, dilation):
+    stride = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
+    padding = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
+    dilation = tuple(dilation) if isinstance(dilation, (tuple, list)) else (dilation, dilation)
+    if tuple(dilation) != (1, 1):
+        # lsq.py:141 unfolds without dilation while lsq.py:382 folds with it; only 1 is consistent
+        raise NotImplementedError("CiM conv supports dilation 1 only (as the reference's unfold)")
+    B, C, H, W = x.shape
+    O, Cw, KH, KW = w.shape
+    if Cw != C:
+        raise ValueError(f"weight in_channels {Cw} != input channels {C} (groups are not supported)")
+    return B, C, H, W, O, KH, KW, stride, padding
+
+
+class get_cim_output_signed(torch.autograd.Function):
+    """HIP implementation of ``get_cim_output_signed`` (lsq.py:89-386)."""
+
+    @staticmethod
+    def forward(ctx, x, w, conv_stride, conv_padding, conv_dilation, act_bits, act_bit_slice,
+                weight_bits, weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim,
+                weight_scaling_factor, act_scaling_factor, stochastic, signed_act):
+        if stochastic:
+            assert adc_bits == 1.5  # lsq.py:136-137
+            raise NotImplementedError("stochastic ADC (lsq.py:205-221) is not implemented on MI355X yet")
+        _require_device(x)
+        dev = x.device
+        B, C, H, W, O, KH, KW, st, pd = _geometry(x, w, conv_stride, conv_padding, conv_dilation)
+        desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, arr, weight_bits, act_bits,
+                              weight_bit_slice, act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ)
+        sizes = _lib.query_sizes(desc)
+        xq = x.detach().to(torch.float32).contiguous()
+        wq = w.detach().to(torch.float32).contiguous()
+        sa = _f32(act_scaling_factor, dev).reshape(-1)[:1].contiguous()
+        sw = _f32(weight_scaling_factor, dev).reshape(-1)[:1].contiguous()
+        bm = binary_mask.detach().to(device=dev, dtype=torch.int8).contiguous()
+        sg = _f32(signed_act, dev).reshape(-1)[:1].contiguous()
+        al = None if alpha_cim is None else alpha_cim.detach().to(device=dev, dtype=torch.float32).contiguous()
+        Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+        Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+        out = torch.empty(B, Ho * Wo, O, device=dev, dtype=torch.float32)
+        cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_forward(desc, xq.data_ptr(), wq.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+                                    None if al is None else al.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                    out.data_ptr(), cbuf.data_ptr(), None, _stream()), "cimq_forward")
+        ctx.desc, ctx.sizes = desc, sizes
+        ctx.bufs = (xq, sa, sw, al, bm, sg, cbuf)
+        ctx.wshape, ctx.xshape = wq.shape, xq.shape
+        ctx.has_alpha = alpha_cim is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        xq, sa, sw, al, bm, sg, cbuf = ctx.bufs
+        dev = xq.device
+        g = grad_output.detach().to(torch.float32).contiguous()
+        gx = torch.empty(ctx.xshape, device=dev, dtype=torch.float32)
+        gw = torch.empty(ctx.wshape, device=dev, dtype=torch.float32)
+        ga = torch.empty_like(al) if (ctx.has_alpha and al is not None) else None
+        ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_backward(ctx.desc, g.data_ptr(), xq.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+                                     None if al is None else al.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                     cbuf.data_ptr(), gx.data_ptr(), gw.data_ptr(),
+                                     None if ga is None else ga.data_ptr(), None, ws.data_ptr(),
+                                     _stream()), "cimq_backward")
+        return (gx, gw) + (None,) * 10 + (ga,) + (None,) * 4
+
+
+class _CimConv2dLSQ(torch.autograd.Function):
+    """Fused LSQ-activation-quantiser + CiM conv (lsq.py:547-549 followed by lsq.py:578)."""
+
+    @staticmethod
+    def forward(ctx, x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding, dilation,
+                nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
+        _require_device(x)
+        dev = x.device
+        B, C, H, W, O, KH, KW, st, pd = _geometry(x, w_q, stride, padding, dilation)
+        qp_a = float(2 ** nbits_a - 1)
+        desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
+                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a)
+        sizes = _lib.query_sizes(desc)
+        xc = x.detach().to(torch.float32).contiguous()
+        wq = w_q.detach().to(torch.float32).contiguous()
+        sa_ = sa.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        sw_ = sw.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        al = None if alpha_q is None else alpha_q.detach().to(torch.float32).contiguous()
+        bm = binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+        sg = signed_act.detach().to(device=dev, dtype=torch.float32).reshape(-1)[:1].contiguous()
+        Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+        Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+        out = torch.empty(B, Ho * Wo, O, device=dev, dtype=torch.float32)
+        cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_forward(desc, xc.data_ptr(), wq.data_ptr(), sa_.data_ptr(), sw_.data_ptr(),
+                                    None if al is None else al.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                    out.data_ptr(), cbuf.data_ptr(), None, _stream()), "cimq_forward")
+        ctx.desc, ctx.sizes = desc, sizes
+        ctx.bufs = (xc, sa_, sw_, al, bm, sg, cbuf)
+        ctx.wshape = wq.shape
+        ctx.has_alpha = alpha_q is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        xc, sa, sw, al, bm, sg, cbuf = ctx.bufs
+        dev = xc.device
+        g = grad_output.detach().to(torch.float32).contiguous()
+        gx = torch.empty_like(xc)
+        gw = torch.empty(ctx.wshape, device=dev, dtype=torch.float32)
+        gsa = torch.empty(1, device=dev, dtype=torch.float32)
+        ga = torch.empty_like(al) if (ctx.has_alpha and al is not None) else None
+        ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_backward(ctx.desc, g.data_ptr(), xc.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+                                     None if al is None else al.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                     cbuf.data_ptr(), gx.data_ptr(), gw.data_ptr(),
+                                     None if ga is None else ga.data_ptr(), gsa.data_ptr(), ws.data_ptr(),
+                                     _stream()), "cimq_backward")
+        return (gx, gw, gsa, None, ga) + (None,) * 11
+
+
+def cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding, dilation,
+                   nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
+    """out[B, P, O] of the fused act-LSQ + CiM conv; differentiable in x, w_q, sa, alpha_q."""
+    return _CimConv2dLSQ.apply(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding,
+                               dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar)
+
+
+def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,
+                   nbits_w, wbitslice, adcbits, xbar, num_xbars):
+    """First-step alpha_cim initialisation on the device (lsq.py:557-563, 35-87)."""
+    _require_device(x)
+    dev = x.device
+    B, C, H, W, O, KH, KW, st, pd = _geometry(x, w_q, stride, padding, (1, 1))
+    desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice, abitslice,
+                          adcbits, _lib.CIMQ_INPUT_RAW_LSQ, float(2 ** nbits_a - 1))
+    sizes = _lib.query_sizes(desc)
+    nbw, nba = int(nbits_w / wbitslice), int(nbits_a / abitslice)
+    out = torch.empty(1, num_xbars, nbw, nba, 1, O, device=dev, dtype=torch.float32)
+    cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+    ws = torch.empty(max(sizes.fwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+    xc = x.detach().to(torch.float32).contiguous()
+    wq = w_q.detach().to(torch.float32).contiguous()
+    sa_ = sa.detach().reshape(-1)[:1].contiguous()
+    sw_ = sw.detach().reshape(-1)[:1].contiguous()
+    bm = binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+    sg = signed_act.detach().to(device=dev, dtype=torch.float32).reshape(-1)[:1].contiguous()
+    lib = _lib.load()
+    _lib.check(lib.cimq_alpha_init(desc, xc.data_ptr(), wq.data_ptr(), sa_.data_ptr(), sw_.data_ptr(),
+                                   bm.data_ptr(), sg.data_ptr(), out.data_ptr(), cbuf.data_ptr(),
+                                   ws.data_ptr(), _stream()), "cimq_alpha_init")
+    return out
+
+
+def debug_partial_sums(x_q, w_q, conv_stride, conv_padding, act_bits, act_bit_slice, weight_bits,
+                       weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim, weight_scaling_factor,
+                       act_scaling_factor, signed_act):
+    """Forward on the device that also returns the integer partial sums [B,T,nbw,nba,P,O]
+    (int32) and the ADC outputs (fp32) -- the reference's ctx.ps_int / adc_out
+    (lsq.py:169-230).  Parity-test hook."""
+    _require_device(x_q)
+    dev = x_q.device
+    B, C, H, W, O, KH, KW, st, pd = _geometry(x_q, w_q, conv_stride, conv_padding, (1, 1))
+    desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, arr, weight_bits, act_bits, weight_bit_slice,
+                          act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ)
+    sizes = _lib.query_sizes(desc)
+    nbw, nba = int(weight_bits / weight_bit_slice), int(act_bits / act_bit_slice)
+    T = int(math.ceil(C * KH * KW / arr))
+    Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+    Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+    out = torch.empty(B, Ho * Wo, O, device=dev, dtype=torch.float32)
+    ps = torch.zeros(B, T, nbw, nba, Ho * Wo, O, device=dev, dtype=torch.int32)
+    adc = torch.zeros(B, T, nbw, nba, Ho * Wo, O, device=dev, dtype=torch.float32)
+    cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+    xq = x_q.detach().float().contiguous()
+    wq = w_q.detach().float().contiguous()
+    sa = _f32(act_scaling_factor, dev).reshape(-1)[:1].contiguous()
+    sw = _f32(weight_scaling_factor, dev).reshape(-1)[:1].contiguous()
+    bm = binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+    sg = _f32(signed_act, dev).reshape(-1)[:1].contiguous()
+    al = None if alpha_cim is None else _f32(alpha_cim, dev)
+    lib = _lib.load()
+    _lib.check(lib.cimq_debug_partial_sums(desc, xq.data_ptr(), wq.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+                                           None if al is None else al.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                           out.data_ptr(), ps.data_ptr(), adc.data_ptr(), cbuf.data_ptr(),
+                                           _stream()), "cimq_debug_partial_sums")
+    return out, ps, adc
+
+
+def logical_macs(B, C, H, W, O, KH, KW, stride, padding) -> int:
+    """ptflops convention B*Ho*Wo*O*C*KH*KW (utils/ptflops/flops_counter.py:314-318)."""
+    Ho = (H + 2 * padding[0] - KH) // stride[0] + 1
+    Wo = (W + 2 * padding[1] - KW) // stride[1] + 1
+    return B * Ho * Wo * O * C * KH * KW
+
+
+def num_xbars(in_channels, kernel_size, xbar) -> int:
+    return int(math.ceil(in_channels * kernel_size[0] * kernel_size[1] / xbar))

@@ -1,0 +1,133 @@
+/*
+ * cimq.h -- C ABI of libcimq.so, the MI355X (gfx950) implementation of the CiM
+ * partial-sum-quantised convolution of UtkarshSaxena1/CiM_Quantization.
+ *
+ * The reference path is pure PyTorch (models/_modules/lsq.py); its device work is
+ * stock torch ops issued from Python.  libcimq replaces that device work with
+ * hand-written CDNA4 HIP kernels.  The Python host layer (cim_quantization_amd)
+ * binds these symbols with ctypes; any other FFI (cgo, JNI, N-API) can bind them the
+ * same way.
+ *
+ * Conventions
+ *  - Every pointer argument is DEVICE memory owned by the caller (e.g. a torch
+ *    tensor's data_ptr()).  The library allocates nothing; scratch comes from the
+ *    caller's ``ws`` of cimq_query_sizes()->*_workspace_bytes.
+ *  - Scalars that live on the device in the reference (the LSQ step sizes sw/sa,
+ *    alpha_cim, signed_act) are passed as device pointers: no host synchronisation.
+ *  - All launches are stream-ordered on ``stream`` (a hipStream_t, passed as void*;
+ *    NULL = the legacy default stream).  Functions are reentrant and keep no global
+ *    mutable state apart from a thread-local error string.
+ *  - Return value: 0 on success, otherwise a CIMQ_E* code; cimq_last_error() gives
+ *    the message.  Nothing throws across the ABI.
+ *
+ * Tensor layouts (identical to the reference):
+ *   x, grad_x      [B, C, H, W]              fp32, NCHW contiguous
+ *   w_q, grad_w    [O, C, KH, KW]            fp32
+ *   out, grad_out  [B, Ho*Wo, O]             fp32 (the Function's [B, P, O] output)
+ *   alpha_q        [1, T, nbw, nba, 1, O]    fp32 (quantised alpha_cim), may be NULL
+ *   binary_mask    [1, 1, nbw, nba, 1, 1]    int8 (wraps for 8-bit layers)
+ *   signed_act     [1]                       fp32 buffer (0 or 1)
+ */
+#ifndef CIMQ_H
+#define CIMQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CIMQ_ABI_VERSION 1
+
+/* status codes */
+#define CIMQ_OK 0
+#define CIMQ_EINVAL 1      /* descriptor / argument rejected */
+#define CIMQ_EUNSUPPORTED 2 /* valid for the reference but not implemented here */
+#define CIMQ_EHIP 3        /* a HIP runtime call failed */
+
+/* what ``x`` holds (cimq_conv_desc.input_kind) */
+#define CIMQ_INPUT_XQ 0     /* x is x_q, the quantised activation handed to the Function (lsq.py:92) */
+#define CIMQ_INPUT_RAW_LSQ 1 /* x is the raw activation; the LSQ act quantiser (lsq.py:547-549) is fused */
+
+typedef struct cimq_conv_desc {
+  int32_t batch, in_channels, in_h, in_w; /* B, C, H, W */
+  int32_t out_channels, kernel_h, kernel_w; /* O, KH, KW (square kernels in the reference) */
+  int32_t stride_h, stride_w, pad_h, pad_w;
+  int32_t xbar;       /* crossbar rows per tile ("arr", lsq.py:166); multiple of 16 */
+  int32_t bits_w, bits_a; /* nbits_w, nbits_a */
+  int32_t bs_w, bs_a; /* weight / activation bit-slice widths */
+  float adc_bits;     /* 0 (fp ADC), 1 (sign), 1.5 (ternary, alpha scaled), >1.5 (multi-level) */
+  int32_t input_kind; /* CIMQ_INPUT_* */
+  float lsq_qp;       /* CIMQ_INPUT_RAW_LSQ: act clamp max Qp_a = 2^bits_a - 1 (Qn_a = 0) */
+  int32_t reserved[4];
+} cimq_conv_desc;
+
+typedef struct cimq_sizes {
+  size_t ctx_bytes;           /* forward -> backward state, caller-owned device memory */
+  size_t fwd_workspace_bytes; /* scratch for cimq_forward / cimq_alpha_init */
+  size_t bwd_workspace_bytes; /* scratch for cimq_backward */
+} cimq_sizes;
+
+/* ABI version of the loaded library (compare with CIMQ_ABI_VERSION). */
+int cimq_abi_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* cimq_last_error(void);
+
+/* Validate a descriptor and report the buffer sizes it needs.
+ * Replaces the geometry bookkeeping of get_cim_output_signed.forward (lsq.py:115-170). */
+int cimq_query_sizes(const cimq_conv_desc* d, cimq_sizes* out);
+
+/* Forward of the CiM conv: act codes + bit slices, implicit-im2col int8 MFMA partial sums
+ * per (tile, w-slice, a-slice), ADC requantisation and shift-and-add.
+ * Replaces get_cim_output_signed.forward (lsq.py:92-237); with CIMQ_INPUT_RAW_LSQ it
+ * also absorbs the activation quantiser of Conv2dLSQCiM.forward (lsq.py:547-549).
+ * out = [B, P, O]; ctx receives what cimq_backward needs (the int8 ctx of lsq.py:99,160
+ * and the parameters that stand in for the fp16 partial sums of lsq.py:192). */
+int cimq_forward(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                 const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                 const float* signed_act, float* out, void* ctx, void* ws, void* stream);
+
+/* Backward of the CiM conv.  Replaces get_cim_output_signed.backward (lsq.py:244-386):
+ *   grad_x     [B,C,H,W]  d loss / d x_q (CIMQ_INPUT_XQ) or d loss / d x through the
+ *                          fused LSQ quantiser (CIMQ_INPUT_RAW_LSQ)
+ *   grad_w     [O,C,KH,KW] d loss / d w_q
+ *   grad_alpha [1,T,nbw,nba,1,O] d loss / d alpha_q (adc 1 / 1.5 only, else may be NULL)
+ *   grad_sa    [1]  CIMQ_INPUT_RAW_LSQ only: d loss / d sa from the LSQ graph (lsq.py:548-549)
+ * ``x``, ``sa``, ``sw``, ``alpha_q``, ``binary_mask``, ``signed_act`` must be the same
+ * buffers (same contents) that were given to cimq_forward with this ctx. */
+int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x, const float* sa,
+                  const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                  const float* signed_act, const void* ctx, float* grad_x, float* grad_w,
+                  float* grad_alpha, float* grad_sa, void* ws, void* stream);
+
+/* First-step alpha_cim initialisation (lsq.py:557-563 with get_analog_partial_sums_signed,
+ * lsq.py:35-87): alpha_init[1,T,nbw,nba,1,O] = 2*mean_{b,p}|ps*sw*sa| / sqrt(Qp_adc), zeros
+ * replaced by sw*sa.  Uses x, w_q, sa, sw like cimq_forward (ctx is scratch here). */
+int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                    const float* sw, const int8_t* binary_mask, const float* signed_act,
+                    float* alpha_init, void* ctx, void* ws, void* stream);
+
+/* Diagnostic / parity hook: cimq_forward that also writes every integer partial sum
+ * ps_out[B,T,nbw,nba,P,O] (int32; the reference keeps them as the fp16 ctx.ps_int of
+ * lsq.py:169-192) and its ADC output adc_out (same shape, fp32, before the shift-and-add
+ * mask: adc_out of lsq.py:197-230).  Used by the bit-exactness tests. */
+int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                            const float* sw, const float* alpha_q, const int8_t* binary_mask,
+                            const float* signed_act, float* out, int32_t* ps_out, float* adc_out,
+                            void* ctx, void* stream);
+
+/* Diagnostic kernel timer.  Until cimq_profile_stop(), every launch of kernel ``kernel_id``
+ * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep) is
+ * bracketed by a hipEvent pair on its launch stream (at most ``max_launches``).  stop()
+ * waits for the last event and returns the summed kernel time, the number of launches and
+ * their summed algorithmic bytes / flops ("Roofline accounting"). */
+int cimq_profile_start(int kernel_id, int max_launches);
+int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, double* algo_flops);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CIMQ_H */

@@ -80,6 +80,7 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
         self.register_buffer("init_state", torch.zeros(1))
         self.register_buffer("signed_act", torch.zeros(1))
         self.register_buffer("init_state_cim", torch.zeros(1))
+        self._state_cache = None  # (parity with the product module; unused here)
 
     def forward(self, x):
         qn_w, qp_w = co.lsq_weight_params(self.nbits_w)
@@ -96,6 +97,10 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
         x_q = _rp((x / sa).clamp(qn_a, qp_a)) * sa
         sw = _gs(self.alpha_weight, 1.0 / math.sqrt(self.weight.numel() * qp_w))
         w_q = _rp((self.weight / sw).clamp(qn_w, qp_w)) * sw
+        if getattr(self, "debug_retain", False):  # tests: keep the LSQ intermediates' grads
+            x_q.retain_grad()
+            w_q.retain_grad()
+            self.dbg = dict(x=x, x_q=x_q, w_q=w_q, sa=sa, sw=sw, qa=(qn_a, qp_a), qw=(qn_w, qp_w))
         if self.training and self.init_state_cim == 0 and self.alpha_cim is not None:
             a0 = co.alpha_cim_init(_np(x_q), _np(w_q), self.stride, self.padding, self.nbits_a,
                                    self.abitslice, self.nbits_w, self.wbitslice, self.xbar,

@@ -212,6 +212,28 @@ def _tiles(K: int, arr: int):
     return t
 
 
+def adc_apply(ps16, adc_bits, alpha_cim, sw, sa):
+    """u = ps*sw*sa (lsq.py:195) and the ADC of lsq.py:197-230 on fp16 partial sums."""
+    qn, qp = adc_range(adc_bits)
+    sa = np.asarray(sa, F32).reshape(1)
+    sw = np.asarray(sw, F32).reshape(1)
+    u = ((np.asarray(ps16).astype(F32) * sw).astype(F32) * sa).astype(F32)
+    with np.errstate(all="ignore"):
+        if adc_bits == 0:                                            # :197
+            adc = u
+        elif adc_bits == 1:                                          # :200
+            adc = (np.sign(u) * np.asarray(alpha_cim, F32)).astype(F32)
+        elif adc_bits == 1.5:                                        # :223-225
+            a = np.asarray(alpha_cim, F32)
+            adc = np.clip(np.rint((u / a).astype(F32)), F32(qn), F32(qp)).astype(F32)
+            adc = (adc * a).astype(F32)
+        else:                                                        # :228-230
+            sws = (sw * sa).astype(F32)
+            adc = np.clip(np.rint((u / sws).astype(F32)), F32(qn), F32(qp)).astype(F32)
+            adc = ((adc * sw).astype(F32) * sa).astype(F32)
+    return u, adc
+
+
 class CimCtx:
     """What the reference saves for backward (lsq.py:99-192)."""
 
@@ -253,20 +275,7 @@ def cim_forward(x_q, w_q, stride, padding, dilation, act_bits, act_bs, w_bits, w
             for kk in range(nbw):
                 ps[:, i, kk, j] = np.matmul(xs[:, j, :, lo:hi], ws[kk, lo:hi, :]).astype(F16)
     ctx.ps16 = ps                                                    # :192
-    u = ((ps.astype(F32) * sw).astype(F32) * sa).astype(F32)         # :195
-    with np.errstate(all="ignore"):
-        if adc_bits == 0:                                            # :197
-            adc = u
-        elif adc_bits == 1:                                          # :200
-            adc = (np.sign(u) * np.asarray(alpha_cim, F32)).astype(F32)
-        elif adc_bits == 1.5:                                        # :223-225
-            a = np.asarray(alpha_cim, F32)
-            adc = np.clip(np.rint((u / a).astype(F32)), F32(qn), F32(qp)).astype(F32)
-            adc = (adc * a).astype(F32)
-        else:                                                        # :228-230
-            sws = (sw * sa).astype(F32)
-            adc = np.clip(np.rint((u / sws).astype(F32)), F32(qn), F32(qp)).astype(F32)
-            adc = ((adc * sw).astype(F32) * sa).astype(F32)
+    u, adc = adc_apply(ps, adc_bits, alpha_cim, sw, sa)
     out = np.sum((adc * binary_mask.astype(F32)).astype(F32), axis=(1, 2, 3), dtype=F32)  # :233
     ctx.meta = dict(stride=tuple(stride), padding=tuple(padding), k=k, C=C, O=O, H=x_q.shape[2],
                     W=x_q.shape[3], nbw=nbw, nba=nba, w_bs=w_bs, act_bs=act_bs, act_bits=act_bits,

@@ -1,0 +1,56 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (ROCm device) and libcimq.so")
+
+
+def golden_manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def function_cases():
+    return sorted(k for k, v in golden_manifest().items() if v["kind"] == "function")
+
+
+def module_cases():
+    return sorted(k for k, v in golden_manifest().items() if v["kind"] == "module")
+
+
+def rel_err(mine, ref, terms=None):
+    """max |mine-ref| / (|ref| + sum|terms|), NaNs must coincide."""
+    mine = np.asarray(mine, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert mine.shape == ref.shape, (mine.shape, ref.shape)
+    nm, nr = np.isnan(mine), np.isnan(ref)
+    assert np.array_equal(nm, nr), "NaN pattern differs"
+    scale = np.abs(ref)
+    if terms is not None:
+        scale = np.maximum(scale, np.asarray(terms, np.float64))
+    d = np.abs(mine - ref)[~nr]
+    s = (scale + 1e-30)[~nr]
+    return float((d / s).max()) if d.size else 0.0
+
+
+@pytest.fixture(scope="session")
+def cuda_device():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")

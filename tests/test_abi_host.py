@@ -1,0 +1,95 @@
+"""CPU: libcimq.so loads, exports every symbol include/cimq.h declares, and validates
+descriptors on the host (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+import cim_quantization_amd._lib as L
+from cim_quantization_amd import build as cimq_build
+
+
+@pytest.fixture(scope="module")
+def lib():
+    cimq_build.build(verbose=False)  # no-op when up to date (hipcc cross-compiles, no GPU needed)
+    return L.load()
+
+
+def header_symbols():
+    with open(os.path.join(REPO, "include", "cimq.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cimq_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert header_symbols() == sorted(L.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    raw = ctypes.CDLL(L.LIB_PATH)
+    for sym in header_symbols():
+        assert hasattr(raw, sym), sym
+    assert lib.cimq_abi_version() == L.ABI_VERSION
+
+
+def test_library_is_gfx950_code_object():
+    data = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def _desc(**kw):
+    base = dict(B=256, C=16, H=32, W=32, O=16, KH=3, KW=3, stride=(1, 1), padding=(1, 1), xbar=128,
+                bits_w=3, bits_a=3, bs_w=1, bs_a=1, adc_bits=1.5)
+    base.update(kw)
+    return L.make_desc(**base)
+
+
+def test_query_sizes_resnet20_s1(lib):
+    s = L.query_sizes(_desc())
+    # ctx holds 4 code bytes + 1 ctx byte per input element plus small weight/param tables
+    nin = 256 * 16 * 32 * 32
+    assert 5 * nin <= s.ctx_bytes < 5 * nin + (1 << 20)
+    assert s.bwd_workspace_bytes > 0
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(xbar=100), 2), (dict(xbar=256), 2), (dict(adc_bits=0.7), 1), (dict(bits_w=0), 1),
+    (dict(B=0), 1), (dict(bits_a=9, bs_a=1), 2), (dict(bs_w=6, bits_w=6), 2),
+])
+def test_query_sizes_rejects(lib, kw, code):
+    d = _desc(**kw)
+    s = L.Sizes()
+    rc = lib.cimq_query_sizes(ctypes.byref(d), ctypes.byref(s))
+    assert rc == code
+    assert lib.cimq_last_error().decode()
+
+
+@pytest.mark.parametrize("adc", [0, 1, 1.5, 4, 6])
+def test_query_sizes_accepts_adc_modes(lib, adc):
+    L.query_sizes(_desc(adc_bits=adc))
+
+
+def test_forward_rejects_null_pointers(lib):
+    d = _desc()
+    rc = lib.cimq_forward(ctypes.byref(d), None, None, None, None, None, None, None, None, None, None, None)
+    assert rc == 1
+
+
+def header_arities():
+    with open(os.path.join(REPO, "include", "cimq.h")) as f:
+        txt = f.read()
+    out = {}
+    for m in re.finditer(r"^\s*(?:int|const char\*)\s+(cimq_\w+)\s*\(([^)]*)\)\s*;", txt, re.M | re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else len(params.split(","))
+    return out
+
+
+def test_ctypes_arity_matches_header(lib):
+    ar = header_arities()
+    assert set(ar) == set(L.EXPORTED_SYMBOLS)
+    for sym, n in ar.items():
+        assert len(getattr(lib, sym).argtypes) == n, sym
