@@ -1,0 +1,243 @@
+#!/usr/bin/env python
+"""Benchmark: ResNet-20 w3a3 CiM conv layers, batch 256 per GPU, on MI355X.
+
+One step = forward + backward of all 19 CiM convolutions of a CIFAR ResNet-20
+(BASELINE.json configs[1]; the first conv is w8a8 as ReplaceModuleTool forces it,
+replace_module.py:83-95), xbar 128, 1.5-bit ADC, followed by the data-parallel gradient
+exchange (one flat RCCL all-reduce bucket, N > 1) and an SGD update of the weights and
+step sizes.  Inputs / grads are synthetic tensors of the layer shapes (no dataset);
+weights are kaiming-normal (resnet.py:43-45).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (metric / value / roofline / cpu_baseline ...).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# (name, in_channels, out_channels, input H=W, stride, bits)
+RESNET20 = [("conv1", 3, 16, 32, 1, 8)]
+RESNET20 += [(f"layer1.{b}.conv{c}", 16, 16, 32, 1, 3) for b in range(3) for c in (1, 2)]
+RESNET20 += [("layer2.0.conv1", 16, 32, 32, 2, 3), ("layer2.0.conv2", 32, 32, 16, 1, 3)]
+RESNET20 += [(f"layer2.{b}.conv{c}", 32, 32, 16, 1, 3) for b in (1, 2) for c in (1, 2)]
+RESNET20 += [("layer3.0.conv1", 32, 64, 16, 2, 3), ("layer3.0.conv2", 64, 64, 8, 1, 3)]
+RESNET20 += [(f"layer3.{b}.conv{c}", 64, 64, 8, 1, 3) for b in (1, 2) for c in (1, 2)]
+XBAR, ADC = 128, 1.5
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def out_hw(h, s):
+    return (h + 2 - 3) // s + 1
+
+
+def macs_per_sample():
+    return sum(out_hw(h, s) ** 2 * o * c * 9 for _, c, o, h, s, _ in RESNET20)
+
+
+def build(device, batch, seed=0):
+    import cim_quantization_amd._modules as my_nn
+    torch.manual_seed(seed)
+    layers, xs, gs = [], [], []
+    gen = torch.Generator().manual_seed(seed + 1)
+    for name, c, o, h, s, nb in RESNET20:
+        m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
+                               abitslice=1, xbar=XBAR, adcbits=ADC, signed_xbar=True, stochastic_quant=False)
+        torch.nn.init.kaiming_normal_(m.weight)
+        layers.append(m.to(device).train())
+        x = torch.randn(batch, c, h, h, generator=gen)
+        if name != "conv1":
+            x = x.relu()  # every later conv sees a post-ReLU (BN+ReLU) activation
+        ho = out_hw(h, s)
+        gy = torch.randn(batch, o, ho, ho, generator=gen) / math.sqrt(batch * o * ho * ho)
+        xs.append(x.to(device))
+        gs.append(gy.to(device))
+    return layers, xs, gs
+
+
+class Trainer:
+    """fwd+bwd over the CiM layers, flat-bucket gradient all-reduce, SGD (examples/__init__.py:184-188:
+    alpha_* excluded from weight decay)."""
+
+    def __init__(self, layers, world):
+        self.layers, self.world = layers, world
+        params = [p for m in layers for p in m.parameters()]
+        n = sum(p.numel() for p in params)
+        dev = params[0].device
+        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in params:  # gradients live in one bucket: one all-reduce per step
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        decay = [p for m in layers for nm, p in m.named_parameters() if not nm.startswith("alpha")]
+        no_decay = [p for m in layers for nm, p in m.named_parameters() if nm.startswith("alpha")]
+        self.opt = torch.optim.SGD([{"params": decay, "weight_decay": 1e-4},
+                                    {"params": no_decay, "weight_decay": 0.0}], lr=0.01, momentum=0.9)
+        self.bucket_mb = n * 4 / 1e6
+
+    def step(self, xs, gs):
+        for m, x, gy in zip(self.layers, xs, gs):
+            m(x).backward(gy)
+        if self.world > 1:
+            dist.all_reduce(self.flat)
+            self.flat.mul_(1.0 / self.world)
+        self.opt.step()
+        self.flat.zero_()
+
+
+def timed(trainer, xs, gs, steps, dev, world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step(xs, gs)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def layer_breakdown(trainer, xs, gs, dev):
+    """Per-layer fwd+bwd ms from events on the compute stream (one untimed pass)."""
+    res = []
+    for m, x, gy, spec in zip(trainer.layers, xs, gs, RESNET20):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        m(x).backward(gy)
+        e1.record()
+        res.append((spec[0], e0, e1))
+    torch.cuda.synchronize(dev)
+    trainer.flat.zero_()
+    return {n: round(a.elapsed_time(b), 4) for n, a, b in res}
+
+
+def cpu_baseline(batch_cpu: int, threads: int):
+    """The numpy oracle (a faithful port of the reference's CPU op sequence) timed on the host:
+    forward + backward of all 19 CiM convs at a bounded batch."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cim_oracle as co
+    rng = np.random.default_rng(0)
+    with threadpool_limits(limits=threads):
+        t = 0.0
+        for name, c, o, h, s, nb in RESNET20:
+            sa = np.array([0.11], np.float32)
+            sw = np.array([0.07], np.float32)
+            qn_w, qp_w = co.lsq_weight_params(nb)
+            x_q = (rng.integers(0, 2 ** nb, (batch_cpu, c, h, h)).astype(np.float32) * sa).astype(np.float32)
+            w_q = (rng.integers(qn_w, qp_w + 1, (o, c, 3, 3)).astype(np.float32) * sw).astype(np.float32)
+            T = math.ceil(c * 9 / XBAR)
+            a = (rng.random((1, T, nb, nb, 1, o)).astype(np.float32) * 3 + 0.1) * np.float32(sa[0] * sw[0])
+            aq = co.alpha_quantize(a.astype(np.float32), 8)
+            bm = co.make_binary_mask(nb, nb, 1, 1)
+            ho = out_hw(h, s)
+            g = rng.standard_normal((batch_cpu, ho * ho, o)).astype(np.float32)
+            t0 = time.perf_counter()
+            _, ctx = co.cim_forward(x_q, w_q, (s, s), (1, 1), (1, 1), nb, 1, nb, 1, ADC, XBAR, bm, aq, sw, sa,
+                                    False, np.zeros(1, np.float32))
+            co.cim_backward(ctx, g)
+            t += time.perf_counter() - t0
+    macs = macs_per_sample() * batch_cpu
+    return dict(value=macs / t, unit="MAC/s", cores=threads, kind="port",
+                sample=f"numpy oracle fwd+bwd of the 19 ResNet-20 CiM convs at batch {batch_cpu} "
+                       f"({t:.2f} s, {threads} BLAS threads; elementwise single-threaded)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--cpu-batch", type=int, default=12)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from cim_quantization_amd import _lib
+    _lib.load()  # fail loudly if the HIP library is missing
+
+    layers, xs, gs = build(dev, args.batch, seed=1234 + rank)
+    tr = Trainer(layers, world)
+    for _ in range(max(1, args.warmup)):  # the first step runs the LSQ / alpha_cim init (lsq.py:532-563)
+        tr.step(xs, gs)
+    torch.cuda.synchronize(dev)
+
+    # pick the dominant libcimq kernel from one untimed profiled step per kernel
+    per_kernel = {}
+    for kname in ("fwd", "bwd_gx", "bwd_gw", "prep_act"):
+        with _lib.KernelTimer(kname) as kt:
+            tr.step(xs, gs)
+        per_kernel[kname] = kt.total_ms
+    dominant = max(per_kernel, key=per_kernel.get)
+
+    with _lib.KernelTimer(dominant, max_launches=len(RESNET20) * args.steps + 8) as kt:
+        elapsed = timed(tr, xs, gs, args.steps, dev, world)
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    breakdown = layer_breakdown(tr, xs, gs, dev)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    macs_step = macs_per_sample() * args.batch * world
+    value = macs_step / (elapsed / args.steps)
+    avg_launch_ms = kt.total_ms / max(kt.launches, 1)
+    achieved = (kt.algo_bytes / max(kt.launches, 1)) / (avg_launch_ms * 1e-3) / 1e9
+    result = {
+        "metric": "quantized-MAC/s + fwd+bwd ms per ResNet-20 w3a3 CiM layer, batch 256",
+        "value": value,
+        "unit": "MAC/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "ms_per_layer_fwd_bwd": ms_per_step / len(RESNET20),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "i8+f32",
+        "data": "synthetic (random-init weights, randn / relu(randn) activations of the layer shapes)",
+        "config": {"workload": "resnet20_w3a3_all_19_cim_convs_fwd_bwd_sgd", "global_batch": args.batch * world,
+                   "per_gpu_batch": args.batch, "xbar": XBAR, "adc_bits": ADC, "first_layer": "w8a8",
+                   "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3)},
+        "roofline": {"bound": "hbm", "kernel": _lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]],
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": None, "avg_launch_us": avg_launch_ms * 1e3, "launches": kt.launches,
+                     "algo_bytes_per_launch": kt.algo_bytes / max(kt.launches, 1),
+                     "algo_tflops": kt.algo_flops / max(kt.launches, 1) / (avg_launch_ms * 1e-3) / 1e12},
+        "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
+        "layer_fwd_bwd_ms": breakdown,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_batch, min(16, os.cpu_count() or 1))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

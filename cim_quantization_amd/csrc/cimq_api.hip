@@ -240,14 +240,14 @@ int prof_begin(int kid, const Geo& g, hipStream_t s) {
   algo_counts(g, kid, &b, &f);
   p.bytes += b;
   p.flops += f;
-  hipEventRecord(p.ev[2 * slot], s);
+  (void)hipEventRecord(p.ev[2 * slot], s);
   return slot;
 }
 void prof_end(int slot, hipStream_t s) {
   if (slot < 0) return;
   Profiler& p = prof();
   std::lock_guard<std::mutex> lk(p.mu);
-  hipEventRecord(p.ev[2 * slot + 1], s);
+  (void)hipEventRecord(p.ev[2 * slot + 1], s);
 }
 
 int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, const float* sw,
@@ -505,7 +505,7 @@ int cimq_profile_start(int kernel_id, int max_launches) {
   p.ev = new hipEvent_t[2 * (size_t)max_launches];
   for (int i = 0; i < 2 * max_launches; ++i) {
     if (hipEventCreate(&p.ev[i]) != hipSuccess) {
-      for (int k = 0; k < i; ++k) hipEventDestroy(p.ev[k]);
+      for (int k = 0; k < i; ++k) (void)hipEventDestroy(p.ev[k]);
       delete[] p.ev;
       p.ev = nullptr;
       return fail(CIMQ_EHIP, "hipEventCreate");
@@ -537,7 +537,7 @@ int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, doubl
   if (launches) *launches = p.n;
   if (algo_bytes) *algo_bytes = p.bytes;
   if (algo_flops) *algo_flops = p.flops;
-  for (int i = 0; i < 2 * p.cap; ++i) hipEventDestroy(p.ev[i]);
+  for (int i = 0; i < 2 * p.cap; ++i) (void)hipEventDestroy(p.ev[i]);
   delete[] p.ev;
   p.ev = nullptr;
   p.kid = KID_NONE;
