@@ -32,18 +32,20 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in sources())
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = True, out: str = OUT, defines=()) -> str:
+    """Compile libcimq.so (``defines``/``out``: experiment variants for tools/, never shipped)."""
+    if not force and out == OUT and up_to_date():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wno-pass-failed",
-           "-o", OUT + ".tmp", os.path.join(CSRC, "cimq_api.hip")]
+           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wno-pass-failed"]
+    cmd += [f"-D{d}" for d in defines]
+    cmd += ["-o", out + ".tmp", os.path.join(CSRC, "cimq_api.hip")]
     if verbose:
         print("[cimq] " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

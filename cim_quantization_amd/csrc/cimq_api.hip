@@ -6,11 +6,12 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 
 #include "../../include/cimq.h"
-#include "cimq_kernels.hip"
+#include "cimq_kernels_v3.hip"
 
 using namespace cimq;
 
@@ -105,17 +106,18 @@ int make_geo(const cimq_conv_desc* d, Geo* out) {
 }
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, total;
+  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, total;
 };
 
 CtxLayout ctx_layout(const Geo& g) {
   CtxLayout L;
   size_t o = 0;
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
-  L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);
-  L.xhat = o; o = align256(o + (size_t)g.Nin);
+  L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);  // forward slice bytes
+  L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
+  L.wtc = o; o = align256(o + (size_t)g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
   L.thi = o; o = align256(o + npar * 4);
   L.tlo = o; o = align256(o + npar * 4);
   L.mlo = o; o = align256(o + npar * 4);
@@ -177,9 +179,73 @@ WsLayout ws_layout(const Geo& g) {
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.FBT * 16 * g.Opad);
   W.ga_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.nbw * g.nba * g.Opad);
-  W.lsq_part = o; o = align256(o + sizeof(float) * kLsqParts);
+  W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * ((g.H + 7) / 8)));
   W.total = o;
   return W;
+}
+
+// ---- v3 fast path (whole-row 64-pixel tiles): patch geometry and LDS budgets ----
+struct Plan3 {
+  bool ok;
+  V3 v;
+  size_t lds_fwd, lds_gx, lds_gw, lds_init;
+};
+
+inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+Plan3 v3_plan(const Geo& g) {
+  Plan3 p;
+  memset(&p, 0, sizeof(p));
+  if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0) return p;
+  if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
+  V3& v = p.v;
+  v.lw = 0;
+  while ((1 << v.lw) < g.Wo) ++v.lw;
+  v.RH = (64 / g.Wo - 1) * g.SH + g.KH;
+  v.WP = g.W + 2 * g.PW;
+  v.RI = std::min(g.H, 8);
+  v.nbands = (g.H + v.RI - 1) / v.RI;
+  v.RHB = 0;
+  v.NPB = 0;
+  for (int band = 0; band < v.nbands; ++band) {
+    const int r0 = band * v.RI, r1 = std::min(g.H, r0 + v.RI);
+    int oh_lo = r0 + g.PH - (g.KH - 1);
+    oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.SH - 1) / g.SH;
+    const int oh_hi = std::min(g.Ho - 1, (r1 - 1 + g.PH) / g.SH);
+    const int nro = oh_hi - oh_lo + 1;
+    if (nro <= 0) return p;
+    v.RHB = std::max(v.RHB, (nro - 1) * g.SH + g.KH);
+    v.NPB = std::max(v.NPB, nro * g.Wo);
+  }
+  v.CB = (g.C + 15) / 16;
+  v.NT = (v.RI * g.W + 15) / 16 * v.CB;
+  if (v.NT > 8 * 4 || g.KH > 3 || g.KW > 3) return p;
+  v.nmt = g.M / 64;
+  const int nkj = g.nbw * g.nba;
+  const size_t ckl = a16((size_t)3 * nkj * 4);
+  const size_t patch = a16((size_t)g.C * v.RH * v.WP * g.NBP);
+  const int nof = std::min(4, g.OB16), nog = std::min(2, g.OB16);
+  const size_t fwd_common = patch + (size_t)g.T * g.KS * 64 * 4 + ckl;
+  const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * 16;
+  const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
+  v.fwd_res = fwd_res <= 80 * 1024 ? 1 : 0;
+  p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
+  p.lds_gx = a16((size_t)g.C * v.RHB * v.WP * g.NBP) + a16((size_t)3 * (v.NPB + 1) * 40 * 2) +
+             a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + (size_t)g.NBLK * g.KS * 1024 + a16((size_t)nkj * g.Opad * 8) +
+             (size_t)g.KS * 64 * 4 + ckl + a16((size_t)g.NBLK * 4) + 64;
+  v.NCG = 0;
+  for (int i = 0; i < g.T; ++i) {
+    const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
+    v.NCG = std::max(v.NCG, c1 - c0 + 1);
+  }
+  const size_t pg = a16((size_t)v.NCG * v.RH * v.WP * g.NBP);
+  const size_t gw_tail = (size_t)g.KS * 64 * 4 + (size_t)g.nbw * nog * g.KS * 1024 + (size_t)nkj * nog * 16 * 16 +
+                         a16((size_t)nkj * 32 * 4) + ckl;
+  p.lds_gw = std::max(pg + a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + gw_tail;
+  p.lds_init = pg + gw_tail;
+  const size_t lim = kLdsMax - 512;
+  p.ok = p.lds_fwd <= lim && p.lds_gx <= lim && p.lds_gw <= lim;
+  return p;
 }
 
 template <typename K>
@@ -260,7 +326,7 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     if (grid > 8192) grid = 8192;
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     hipLaunchKernelGGL(prep_act_kernel, dim3(grid), dim3(blk), 0, s, g, x, sa, signed_act,
-                       reinterpret_cast<int8_t*>(ctx + L.xcode), reinterpret_cast<int8_t*>(ctx + L.xhat));
+                       ctx + L.xcode, ctx + L.xhat);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("prep_act"));
   }
@@ -274,6 +340,10 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     int total = g.T * g.FBT * g.NKS * 64;
     hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
                        reinterpret_cast<v4i*>(ctx + L.wgx));
+    const int Cp = (g.C + 15) / 16 * 16;
+    const int tw = g.KHW * Cp * g.NKS * 4;
+    hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
+                       reinterpret_cast<uint4*>(ctx + L.wtc));
     CIMQ_TRY(check_hip("prep_wgx"));
   }
   Params pp = params_of(g, ctx);
@@ -287,14 +357,33 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   return CIMQ_OK;
 }
 
+template <int NBP, int KS>
+int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
+                  hipStream_t s) {
+  CtxLayout L = ctx_layout(g);
+  auto kern = cim_fwd_v3_kernel<NBP, KS>;
+  CIMQ_TRY(set_lds(kern, p.lds_fwd));
+  dim3 grid(std::min(p.v.nmt, 2048), cdiv(g.OB16, 4));
+  const int slot = prof_begin(KID_FWD, g, s);
+  hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
+                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out);
+  prof_end(slot, s);
+  return check_hip("cim_fwd_v3");
+}
+
 template <int NBP, bool DBG>
 int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
                float* adc_dbg, hipStream_t s) {
   CtxLayout L = ctx_layout(g);
+  const Plan3 p = v3_plan(g);
+  if (p.ok && !DBG) {
+    if (g.KS == 1) return launch_fwd_v3<NBP, 1>(g, p, ctx, sw, sa, out, s);
+    return launch_fwd_v3<NBP, 2>(g, p, ctx, sw, sa, out, s);
+  }
+  dim3 grid(cdiv(g.M, 64), cdiv(g.OB16, 4));
   const size_t lds = lds_tile(g);
   auto kern = cim_fwd_kernel<NBP, DBG>;
   CIMQ_TRY(set_lds(kern, lds));
-  dim3 grid(cdiv(g.M, 64), cdiv(g.OB16, 4));
   const int slot = DBG ? -1 : prof_begin(KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
                      reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ps_dbg,
@@ -308,27 +397,62 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
               const float* gout, uint8_t* ws, hipStream_t s) {
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
-  const size_t lds = lds_gw(g);
-  auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;
-  CIMQ_TRY(set_lds(kern, lds));
+  const Plan3 p = v3_plan(g);
+  Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   dim3 grid(W.nchunks, g.T, (g.OB16 + 1) / 2);
   const int slot = INIT ? -1 : prof_begin(KID_BWD_GW, g, s);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
-                     reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(ctx + L.wfrag),
-                     params_of(g, const_cast<uint8_t*>(ctx)), sw, sa, signed_act, gout, W.rows,
-                     reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
+  if (p.ok) {
+    const size_t lds = INIT ? p.lds_init : p.lds_gw;
+    auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, INIT> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, INIT>;
+    CIMQ_TRY(set_lds(kern, lds));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
+                       reinterpret_cast<const v4i*>(ctx + L.wfrag), pp, sw, sa, gout, W.rows,
+                       reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
+  } else {
+    const size_t lds = lds_gw(g);
+    auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;
+    CIMQ_TRY(set_lds(kern, lds));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
+                       reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(ctx + L.wfrag),
+                       pp, sw, sa, signed_act, gout, W.rows, reinterpret_cast<float*>(ws + W.gw_slab),
+                       reinterpret_cast<float*>(ws + W.ga_slab));
+  }
   prof_end(slot, s);
   return check_hip("cim_bwd_gw");
 }
 
+// grad_x; returns through *lsq_fused whether the LSQ activation backward was applied
 template <int NBP, int FBMAX>
 int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
-              float* gx, hipStream_t s) {
+              const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused) {
   CtxLayout L = ctx_layout(g);
-  const int8_t* xc = reinterpret_cast<const int8_t*>(ctx + L.xcode);
+  WsLayout W = ws_layout(g);
+  const Plan3 p = v3_plan(g);
   const v4i* wf = reinterpret_cast<const v4i*>(ctx + L.wfrag);
   const v4i* wg = reinterpret_cast<const v4i*>(ctx + L.wgx);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
+  *lsq_fused = false;
+  if (p.ok) {
+    const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
+    float* part = reinterpret_cast<float*>(ws + W.lsq_part);
+    dim3 grid(g.B * p.v.nbands);
+    auto kern = cim_bwd_gx_v4_kernel<NBP, 2, 4, true>;
+    if (p.v.NT <= 16) {
+      if (lsq) kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 2, true> : cim_bwd_gx_v4_kernel<NBP, 2, 2, true>;
+      else kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 2, false> : cim_bwd_gx_v4_kernel<NBP, 2, 2, false>;
+    } else {
+      if (lsq) kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 4, true> : cim_bwd_gx_v4_kernel<NBP, 2, 4, true>;
+      else kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 4, false> : cim_bwd_gx_v4_kernel<NBP, 2, 4, false>;
+    }
+    CIMQ_TRY(set_lds(kern, p.lds_gx));
+    const int slot = prof_begin(KID_BWD_GX, g, s);
+    hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx, s, g, p.v, ctx + L.xcode, wf,
+                       reinterpret_cast<const uint4*>(ctx + L.wtc), pp, sw, sa, gout, x, gx, part);
+    prof_end(slot, s);
+    *lsq_fused = lsq;
+    return check_hip("cim_bwd_gx_v3");
+  }
+  const int8_t* xc = reinterpret_cast<const int8_t*>(ctx + L.xcode);
   if (gx_lds_ok(g)) {
     const size_t lds = lds_tile(g) + sizeof(float) * g.C * g.HW;
     auto kern = cim_bwd_gx_kernel<NBP, FBMAX, true>;
@@ -354,17 +478,18 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
 
 template <int NBP, int FBMAX>
 int launch_bwd_all(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
-                   const float* signed_act, const float* gout, float* gx, uint8_t* ws, hipStream_t s) {
-  CIMQ_TRY((launch_gx<NBP, FBMAX>(g, ctx, sw, sa, gout, gx, s)));
+                   const float* signed_act, const float* gout, const float* x, float* gx, uint8_t* ws,
+                   hipStream_t s, bool* lsq_fused) {
+  CIMQ_TRY((launch_gx<NBP, FBMAX>(g, ctx, sw, sa, gout, x, gx, ws, s, lsq_fused)));
   CIMQ_TRY((launch_gw<NBP, FBMAX, false>(g, ctx, sw, sa, signed_act, gout, ws, s)));
   return CIMQ_OK;
 }
 
 template <int NBP>
-int dispatch_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
-                 const float* signed_act, const float* gout, float* gx, uint8_t* ws, hipStream_t s) {
-  if (g.FBT <= 4) return launch_bwd_all<NBP, 4>(g, ctx, sw, sa, signed_act, gout, gx, ws, s);
-  return launch_bwd_all<NBP, 8>(g, ctx, sw, sa, signed_act, gout, gx, ws, s);
+int dispatch_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
+                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused) {
+  if (g.FBT <= 4) return launch_bwd_all<NBP, 4>(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
+  return launch_bwd_all<NBP, 8>(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
 }
 
 template <int NBP>
@@ -372,6 +497,16 @@ int dispatch_init(const Geo& g, const uint8_t* ctx, const float* sw, const float
                   const float* signed_act, uint8_t* ws, hipStream_t s) {
   if (g.FBT <= 4) return launch_gw<NBP, 4, true>(g, ctx, sw, sa, signed_act, nullptr, ws, s);
   return launch_gw<NBP, 8, true>(g, ctx, sw, sa, signed_act, nullptr, ws, s);
+}
+
+int launch_reduce_galpha(const Geo& g, const uint8_t* ctx, uint8_t* ws, float cgrad, int init, const float* sw,
+                         const float* sa, float* out, hipStream_t s) {
+  WsLayout W = ws_layout(g);
+  const long long nout = (long long)g.T * g.nbw * g.nba * g.Opad;
+  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(256), 0, s, g, W.nchunks,
+                     reinterpret_cast<const float*>(ws + W.ga_slab), params_of(g, const_cast<uint8_t*>(ctx)),
+                     cgrad, init, sw, sa, (float)((double)g.B * g.P), (float)sqrt((double)g.qp), out);
+  return check_hip("reduce_galpha");
 }
 
 }  // namespace
@@ -441,27 +576,34 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
   uint8_t* w = reinterpret_cast<uint8_t*>(ws);
-  if (g.NBP == 4) CIMQ_TRY(dispatch_bwd<4>(g, c, sw, sa, signed_act, grad_out, grad_x, w, s));
-  else CIMQ_TRY(dispatch_bwd<8>(g, c, sw, sa, signed_act, grad_out, grad_x, w, s));
+  bool lsq_fused = false;
+  if (g.NBP == 4) CIMQ_TRY(dispatch_bwd<4>(g, c, sw, sa, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
+  else CIMQ_TRY(dispatch_bwd<8>(g, c, sw, sa, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
   WsLayout W = ws_layout(g);
-  hipLaunchKernelGGL(reduce_gw_kernel, dim3(cdiv((long long)g.O * g.K, 256)), dim3(256), 0, s, g, W.nchunks,
-                     reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
-  CIMQ_TRY(check_hip("reduce_gw"));
+  {
+    const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
+    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(256), 0, s, g, W.nchunks,
+                       reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
+    CIMQ_TRY(check_hip("reduce_gw"));
+  }
   if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && grad_alpha) {
     const double numel = (double)g.B * g.T * g.nbw * g.nba * g.P * g.O;
     const float cgrad = (float)(1.0 / sqrt(numel * (double)g.qp));  // lsq.py:323,330
-    hipLaunchKernelGGL(reduce_galpha_kernel, dim3(cdiv((long long)g.T * g.nbw * g.nba * g.O, 256)), dim3(256), 0,
-                       s, g, W.nchunks, reinterpret_cast<const float*>(w + W.ga_slab),
-                       params_of(g, const_cast<uint8_t*>(c)), cgrad, grad_alpha);
-    CIMQ_TRY(check_hip("reduce_galpha"));
+    CIMQ_TRY(launch_reduce_galpha(g, c, w, cgrad, 0, sw, sa, grad_alpha, s));
   }
   if (g.input_kind == CIMQ_INPUT_RAW_LSQ) {
-    int grid = cdiv(g.Nin, 256);
-    if (grid > kLsqParts) grid = kLsqParts;
     float* part = reinterpret_cast<float*>(w + W.lsq_part);
-    hipLaunchKernelGGL(lsq_act_bwd_kernel, dim3(grid), dim3(256), 0, s, g.Nin, x, sa, g.lsq_qp, grad_x, part);
-    CIMQ_TRY(check_hip("lsq_act_bwd"));
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, grid, part, grad_sa);
+    int nparts;
+    if (lsq_fused) {
+      nparts = g.B * v3_plan(g).v.nbands;
+    } else {
+      int grid = cdiv(g.Nin, 256);
+      if (grid > kLsqParts) grid = kLsqParts;
+      hipLaunchKernelGGL(lsq_act_bwd_kernel, dim3(grid), dim3(256), 0, s, g.Nin, x, sa, g.lsq_qp, grad_x, part);
+      CIMQ_TRY(check_hip("lsq_act_bwd"));
+      nparts = grid;
+    }
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, nparts, part, grad_sa);
     CIMQ_TRY(check_hip("sum_partials"));
   }
   return CIMQ_OK;
@@ -483,17 +625,12 @@ int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, c
   // negative there, so the signed and unsigned slicings coincide
   CIMQ_TRY(prep_all(g, x, w_q, sa, sw, nullptr, binary_mask, signed_act, c, s, false, false));
   {
-    // ckj (mask floats) are not needed by INIT; flags must read 0
     Params pp = params_of(g, c);
     if (hipMemsetAsync(pp.flags, 0, 16, s) != hipSuccess) return fail(CIMQ_EHIP, "memset flags");
   }
   if (g.NBP == 4) CIMQ_TRY(dispatch_init<4>(g, c, sw, sa, signed_act, w, s));
   else CIMQ_TRY(dispatch_init<8>(g, c, sw, sa, signed_act, w, s));
-  WsLayout W = ws_layout(g);
-  hipLaunchKernelGGL(reduce_alpha_init_kernel, dim3(cdiv((long long)g.T * g.nbw * g.nba * g.O, 256)), dim3(256), 0,
-                     s, g, W.nchunks, reinterpret_cast<const float*>(w + W.ga_slab), sw, sa,
-                     (float)((double)g.B * g.P), (float)sqrt((double)g.qp), alpha_init);
-  return check_hip("reduce_alpha_init");
+  return launch_reduce_galpha(g, c, w, 0.f, 1, sw, sa, alpha_init, s);
 }
 
 int cimq_profile_start(int kernel_id, int max_launches) {

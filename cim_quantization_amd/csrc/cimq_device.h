@@ -35,8 +35,8 @@ struct Geo {
 struct Params {
   int* thi;     // forward: ps >= thi -> code +1   (ternary mode)
   int* tlo;     // forward: ps <= tlo -> code -1
-  int* mlo;     // backward: STE passes iff mlo <= ps <= mhi  (lsq.py:310-313)
-  int* mhi;
+  int* mlo;     // backward: STE passes iff (unsigned)(ps - mlo) <= (unsigned)mhi (lsq.py:310-313)
+  int* mhi;     //   ... mhi holds the interval span
   float* coef;  // alpha_q * binary_mask  (ternary / sign)
   float* alpha; // alpha_q (literal paths)
   float* ckj;   // [3][nbw*nba]: mask as float, cE = 2^-(bsa*j)*mask, cD = 2^-(bsw*k)*mask

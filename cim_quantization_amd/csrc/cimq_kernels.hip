@@ -20,15 +20,31 @@ namespace cimq {
 #define WAVE 64
 
 // =========================================================================================
-// prep_act: per input element, the forward bit-slice integers and the int8 backward code
+// prep_act: per input element, the forward bit-slice integers and the backward ctx slices
 // =========================================================================================
 // x_int = x_q / sa (lsq.py:97); with RAW_LSQ, x_q = round_pass(clamp(x/sa,0,Qp))*sa first
 // (lsq.py:549).  Forward slices follow slicing_act / slicing_act_signed on x_int
 // (lsq.py:146-149) and are stored as rint() int8s (|residue| << 0.5, so the int8 MAC gives
-// round(ps_ref)); ctx code = int8(x_int) (lsq.py:99, truncation + wrap).
+// round(ps_ref)).  Backward slices are those of the int8 ctx code int8(x_int) (lsq.py:99,
+// truncation + wrap) as re-sliced by the backward (lsq.py:290-295).  Both are written as
+// NBP-byte words per element (byte j = slice j), once, so no kernel re-slices per gather.
+__device__ inline void pack_word(int8_t (&v)[8], int nbp, uint8_t* dst, long long idx) {
+  uint32_t lo = (uint8_t)v[0] | ((uint32_t)(uint8_t)v[1] << 8) | ((uint32_t)(uint8_t)v[2] << 16) |
+                ((uint32_t)(uint8_t)v[3] << 24);
+  if (nbp == 4) {
+    reinterpret_cast<uint32_t*>(dst)[idx] = lo;
+  } else {
+    uint2 w;
+    w.x = lo;
+    w.y = (uint8_t)v[4] | ((uint32_t)(uint8_t)v[5] << 8) | ((uint32_t)(uint8_t)v[6] << 16) |
+          ((uint32_t)(uint8_t)v[7] << 24);
+    reinterpret_cast<uint2*>(dst)[idx] = w;
+  }
+}
+
 __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ sa_p,
-                                const float* __restrict__ signed_p, int8_t* __restrict__ xcode,
-                                int8_t* __restrict__ xhat) {
+                                const float* __restrict__ signed_p, uint8_t* __restrict__ xcf,
+                                uint8_t* __restrict__ xcb) {
   const float sa = *sa_p;
   const bool sgn = (*signed_p) != 0.f;
   const long long n = g.Nin;
@@ -45,27 +61,21 @@ __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float*
     } else {
       xq = v;
     }
-    float xi = xq / sa;
-    xhat[idx] = (int8_t)to_i8_wrap(xi);
-    int8_t out[8];
+    const float xi = xq / sa;
+    const float xh = (float)to_i8_wrap(xi);
+    int8_t fw[8], bw[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float s = 0.f;
-      if (j < g.nba) s = sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa);
-      out[j] = (j < g.nba) ? (int8_t)clamp_i8(s) : (int8_t)0;
+      float s = 0.f, sb = 0.f;
+      if (j < g.nba) {
+        s = sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa);
+        sb = sgn ? slice_signed(xh, j, g.bsa) : slice_unsigned(xh, j, g.bsa);
+      }
+      fw[j] = (j < g.nba) ? (int8_t)clamp_i8(s) : (int8_t)0;
+      bw[j] = (j < g.nba) ? (int8_t)clamp_i8(sb) : (int8_t)0;
     }
-    if (g.NBP == 4) {
-      uint32_t w = (uint8_t)out[0] | ((uint32_t)(uint8_t)out[1] << 8) |
-                   ((uint32_t)(uint8_t)out[2] << 16) | ((uint32_t)(uint8_t)out[3] << 24);
-      reinterpret_cast<uint32_t*>(xcode)[idx] = w;
-    } else {
-      uint2 w;
-      w.x = (uint8_t)out[0] | ((uint32_t)(uint8_t)out[1] << 8) | ((uint32_t)(uint8_t)out[2] << 16) |
-            ((uint32_t)(uint8_t)out[3] << 24);
-      w.y = (uint8_t)out[4] | ((uint32_t)(uint8_t)out[5] << 8) | ((uint32_t)(uint8_t)out[6] << 16) |
-            ((uint32_t)(uint8_t)out[7] << 24);
-      reinterpret_cast<uint2*>(xcode)[idx] = w;
-    }
+    pack_word(fw, g.NBP, xcf, idx);
+    pack_word(bw, g.NBP, xcb, idx);
   }
 }
 
@@ -138,6 +148,29 @@ __global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const floa
     v4i o;
     o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
     wgx[t] = o;
+  }
+}
+
+// grad_x transposed-GEMM operand: int8(slice) as bf16 in [khw][c (Cp)][kappa (NKS*32)] order,
+// wtc row (khw, c) = weight row f = c*KHW + khw, so one 16-B piece holds 8 consecutive kappa.
+__global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,
+                                uint4* __restrict__ wtc) {
+  const float sw = *sw_p;
+  const int KAP = g.NKS * 32;
+  const int total = g.KHW * Cp * (KAP / 8);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int piece = t % (KAP / 8), row = t / (KAP / 8);
+    const int khw = row / Cp, c = row - khw * Cp;
+    const int f = c * g.KHW + khw;
+    uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kap = piece * 8 + e;
+      float val = 0.f;
+      if (c < g.C && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, w_q, sw, f, kap));
+      wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
+    }
+    wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
   }
 }
 
@@ -229,8 +262,9 @@ __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, con
     }
     pp.thi[t] = thi;
     pp.tlo[t] = tlo;
-    pp.mlo[t] = mlo;
-    pp.mhi[t] = mhi;
+    // STE interval as (lo, span): pass <=> (unsigned)(ps - lo) <= (unsigned)span
+    if (mhi >= mlo) { pp.mlo[t] = mlo; pp.mhi[t] = mhi - mlo; }
+    else { pp.mlo[t] = -(1 << 30); pp.mhi[t] = 0; }
     if (literal) atomicOr(&pp.flags[0], 1);
   }
 }
@@ -543,7 +577,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __
               for (int r = 0; r < 4; ++r) {
                 bool pass;
                 if (!literal) {
-                  pass = (acc[r] >= pp.mlo[pi + r]) && (acc[r] <= pp.mhi[pi + r]);
+                  pass = (unsigned)(acc[r] - pp.mlo[pi + r]) <= (unsigned)pp.mhi[pi + r];
                 } else {
                   const float b = psb_literal(acc[r], g.mode, sw, sa, pp.alpha[pi + r]);
                   pass = ste_pass(b, g.thr_hi, g.thr_lo);
@@ -678,7 +712,6 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const int mc = blockIdx.x;
   const int mbeg = mc * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
   const float sw = *sw_p, sa = *sa_p;
-  const bool sgn = (*signed_p) != 0.f;
   const bool literal = (pp.flags[0] != 0);
   const bool ternary_fast = (!literal) && g.mode == ADC_TERNARY;
   const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
@@ -705,17 +738,12 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int4 ri = sm.rowinfo[rq + e];
-          float xv = 0.f;
-          if (fk >= 0 && ri.w) {
-            const int ih = ri.y + (fk >> 16), iw = ri.z + (fk & 0xFFFF);
-            if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) xv = (float)xhat[(size_t)ri.x + sm.foff[t]];
-          }
+          const uint2 c = gather_code<NBP>(g, xhat, ri, sm.foff[t], fk);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (j < g.nba) {
-              const float s = sgn ? slice_signed(xv, j, g.bsa) : slice_unsigned(xv, j, g.bsa);
-              pl[j] |= ((uint32_t)(uint8_t)(int8_t)clamp_i8(s)) << (8 * e);
-            }
+          for (int j = 0; j < 4; ++j) pl[j] |= ((c.x >> (8 * j)) & 0xFFu) << (8 * e);
+          if (NBP == 8) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pl[4 + j] |= ((c.y >> (8 * j)) & 0xFFu) << (8 * e);
           }
         }
 #pragma unroll
@@ -773,7 +801,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
 #pragma unroll
                   for (int r = 0; r < 4; ++r) {
                     const int p = acc[r];
-                    D[j][r] += ((p >= mlo) && (p <= mhi)) ? cd : 0.f;
+                    D[j][r] += ((unsigned)(p - mlo) <= (unsigned)mhi) ? cd : 0.f;
                     const float q = (p >= thi) ? 1.f : ((p <= tlo) ? -1.f : 0.f);
                     qs += q * gval[r];
                   }
@@ -784,7 +812,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                   for (int r = 0; r < 4; ++r) {
                     const int p = acc[r];
                     const float b = psb_literal(p, g.mode, sw, sa, al);
-                    const bool pass = literal ? ste_pass(b, g.thr_hi, g.thr_lo) : ((p >= mlo) && (p <= mhi));
+                    const bool pass = literal ? ste_pass(b, g.thr_hi, g.thr_lo) : ((unsigned)(p - mlo) <= (unsigned)mhi);
                     D[j][r] += pass ? cd : 0.f;
                     if (has_code) qs += alpha_code_literal(b, g.mode, g.qn, g.qp, g.thr_hi, g.thr_lo) * gval[r];
                   }

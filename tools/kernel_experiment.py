@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Time libcimq kernels of one ResNet-20 layer shape for several experiment builds.
+
+    python tools/kernel_experiment.py --build            # (CPU) compile the variant libraries
+    python tools/kernel_experiment.py --layer layer1.0.conv1   # (GPU) time them
+
+Variant libraries live in exp/ (git-ignored); they skip parts of a kernel to attribute its
+time and give wrong results by design -- never used by the product path or the tests.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+# name -> preprocessor defines; kernels carry CIMQ_EXP_* knobs only while an experiment runs
+VARIANTS = {
+    "base": [],
+}
+
+
+def lib_path(name):
+    return os.path.join(REPO, "exp", f"libcimq_{name}.so")
+
+
+def do_build():
+    from cim_quantization_amd import build as B
+    os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
+    with cf.ThreadPoolExecutor(len(VARIANTS)) as ex:
+        futs = {ex.submit(B.build, True, False, lib_path(n), d): n for n, d in VARIANTS.items()}
+        for f in cf.as_completed(futs):
+            f.result()
+            print("built", futs[f], flush=True)
+
+
+def do_time(layer, iters):
+    import torch
+    import bench
+    from cim_quantization_amd import _lib
+    names = [r[0] for r in bench.RESNET20]
+    bench.RESNET20[:] = [bench.RESNET20[names.index(layer)]]
+    layers, xs, gs = bench.build(torch.device("cuda:0"), 256)
+    m, x, g = layers[0], xs[0], gs[0]
+    for name in VARIANTS:
+        _lib._lib = _lib.load(lib_path(name))
+        x1 = x.detach().requires_grad_(True)
+        m(x1).backward(g)  # warm (alpha init etc.)
+        torch.cuda.synchronize()
+        res = {}
+        for kern in ("fwd", "bwd_gx", "bwd_gw"):
+            with _lib.KernelTimer(kern) as kt:
+                for _ in range(iters):
+                    x1 = x.detach().requires_grad_(True)
+                    m(x1).backward(g)
+                torch.cuda.synchronize()
+            res[kern] = kt.total_ms / max(kt.launches, 1) * 1000
+        print(f"{layer:16s} {name:10s} " + "  ".join(f"{k}={v:8.1f}us" for k, v in res.items()), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--layer", action="append")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    if a.build:
+        do_build()
+    else:
+        for L in a.layer or ["layer1.0.conv1"]:
+            do_time(L, a.iters)
