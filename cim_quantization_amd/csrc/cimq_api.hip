@@ -106,7 +106,7 @@ int make_geo(const cimq_conv_desc* d, Geo* out) {
 }
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, total;
+  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st, total;
 };
 
 CtxLayout ctx_layout(const Geo& g) {
@@ -126,6 +126,8 @@ CtxLayout ctx_layout(const Geo& g) {
   L.alpha = o; o = align256(o + npar * 4);
   L.ckj = o; o = align256(o + 3 * 64 * 4);
   L.flags = o; o = align256(o + 16);
+  // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
+  L.st = o; o = align256(o + (size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4));
   L.total = o;
   return L;
 }
@@ -196,7 +198,8 @@ inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
 Plan3 v3_plan(const Geo& g) {
   Plan3 p;
   memset(&p, 0, sizeof(p));
-  if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0) return p;
+  if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0 || g.Wo < 4) return p;
+  if (g.O > 256 || 256 % g.O != 0) return p;  // grad_alpha reducer: one thread per channel
   if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
   V3& v = p.v;
   v.lw = 0;
@@ -226,13 +229,11 @@ Plan3 v3_plan(const Geo& g) {
   const size_t patch = a16((size_t)g.C * v.RH * v.WP * g.NBP);
   const int nof = std::min(4, g.OB16), nog = std::min(2, g.OB16);
   const size_t fwd_common = patch + (size_t)g.T * g.KS * 64 * 4 + ckl;
-  const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * 16;
+  const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * (16 + 4);
   const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
   v.fwd_res = fwd_res <= 80 * 1024 ? 1 : 0;
   p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
-  p.lds_gx = a16((size_t)g.C * v.RHB * v.WP * g.NBP) + a16((size_t)3 * (v.NPB + 1) * 40 * 2) +
-             a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + (size_t)g.NBLK * g.KS * 1024 + a16((size_t)nkj * g.Opad * 8) +
-             (size_t)g.KS * 64 * 4 + ckl + a16((size_t)g.NBLK * 4) + 64;
+  p.lds_gx = a16((size_t)3 * (v.NPB + 1) * 32 * 2) + a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + ckl + 64;
   v.NCG = 0;
   for (int i = 0; i < g.T; ++i) {
     const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
@@ -241,7 +242,7 @@ Plan3 v3_plan(const Geo& g) {
   const size_t pg = a16((size_t)v.NCG * v.RH * v.WP * g.NBP);
   const size_t gw_tail = (size_t)g.KS * 64 * 4 + (size_t)g.nbw * nog * g.KS * 1024 + (size_t)nkj * nog * 16 * 16 +
                          a16((size_t)nkj * 32 * 4) + ckl;
-  p.lds_gw = std::max(pg + a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + gw_tail;
+  p.lds_gw = std::max(a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + 128 * 4 + ckl;
   p.lds_init = pg + gw_tail;
   const size_t lim = kLdsMax - 512;
   p.ok = p.lds_fwd <= lim && p.lds_gx <= lim && p.lds_gw <= lim;
@@ -366,7 +367,7 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   dim3 grid(std::min(p.v.nmt, 2048), cdiv(g.OB16, 4));
   const int slot = prof_begin(KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
-                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out);
+                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);
   prof_end(slot, s);
   return check_hip("cim_fwd_v3");
 }
@@ -379,6 +380,12 @@ int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, flo
   if (p.ok && !DBG) {
     if (g.KS == 1) return launch_fwd_v3<NBP, 1>(g, p, ctx, sw, sa, out, s);
     return launch_fwd_v3<NBP, 2>(g, p, ctx, sw, sa, out, s);
+  }
+  if (p.ok) {
+    // the debug forward is the general kernel; the fast one still fills the state words the
+    // fast backward reads (same out values)
+    if (g.KS == 1) CIMQ_TRY((launch_fwd_v3<NBP, 1>(g, p, ctx, sw, sa, out, s)));
+    else CIMQ_TRY((launch_fwd_v3<NBP, 2>(g, p, ctx, sw, sa, out, s)));
   }
   dim3 grid(cdiv(g.M, 64), cdiv(g.OB16, 4));
   const size_t lds = lds_tile(g);
@@ -401,8 +408,21 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   dim3 grid(W.nchunks, g.T, (g.OB16 + 1) / 2);
   const int slot = INIT ? -1 : prof_begin(KID_BWD_GW, g, s);
-  if (p.ok) {
-    const size_t lds = INIT ? p.lds_init : p.lds_gw;
+  if (p.ok && !INIT) {
+    auto kern = g.nbw <= 4 ? cim_bwd_gw_v5_kernel<NBP, FBMAX, 4> : cim_bwd_gw_v5_kernel<NBP, FBMAX, 8>;
+    CIMQ_TRY(set_lds(kern, p.lds_gw));
+    dim3 grid16(W.nchunks, g.T, g.OB16);
+    hipLaunchKernelGGL(kern, grid16, dim3(256), p.lds_gw, s, g, p.v, ctx + L.st, ctx + L.xhat, pp, gout, W.rows,
+                       reinterpret_cast<float*>(ws + W.gw_slab));
+    prof_end(slot, s);
+    CIMQ_TRY(check_hip("cim_bwd_gw_v5"));
+    if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
+      hipLaunchKernelGGL(cim_galpha_v5_kernel<NBP>, dim3(W.nchunks, g.T * g.nbw), dim3(256), 0, s, g, ctx + L.st,
+                         gout, W.rows, reinterpret_cast<float*>(ws + W.ga_slab));
+    }
+    return check_hip("cim_galpha_v5");
+  } else if (p.ok) {
+    const size_t lds = p.lds_init;
     auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, INIT> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, INIT>;
     CIMQ_TRY(set_lds(kern, lds));
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
@@ -436,21 +456,16 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     float* part = reinterpret_cast<float*>(ws + W.lsq_part);
     dim3 grid(g.B * p.v.nbands);
-    auto kern = cim_bwd_gx_v4_kernel<NBP, 2, 4, true>;
-    if (p.v.NT <= 16) {
-      if (lsq) kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 2, true> : cim_bwd_gx_v4_kernel<NBP, 2, 2, true>;
-      else kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 2, false> : cim_bwd_gx_v4_kernel<NBP, 2, 2, false>;
-    } else {
-      if (lsq) kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 4, true> : cim_bwd_gx_v4_kernel<NBP, 2, 4, true>;
-      else kern = g.KS == 1 ? cim_bwd_gx_v4_kernel<NBP, 1, 4, false> : cim_bwd_gx_v4_kernel<NBP, 2, 4, false>;
-    }
+    auto kern = cim_bwd_gx_v5_kernel<NBP, 2, true>;
+    if (p.v.NT <= 16) kern = lsq ? cim_bwd_gx_v5_kernel<NBP, 2, true> : cim_bwd_gx_v5_kernel<NBP, 2, false>;
+    else kern = lsq ? cim_bwd_gx_v5_kernel<NBP, 4, true> : cim_bwd_gx_v5_kernel<NBP, 4, false>;
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_BWD_GX, g, s);
-    hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx, s, g, p.v, ctx + L.xcode, wf,
+    hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx, s, g, p.v, ctx + L.st,
                        reinterpret_cast<const uint4*>(ctx + L.wtc), pp, sw, sa, gout, x, gx, part);
     prof_end(slot, s);
     *lsq_fused = lsq;
-    return check_hip("cim_bwd_gx_v3");
+    return check_hip("cim_bwd_gx_v5");
   }
   const int8_t* xc = reinterpret_cast<const int8_t*>(ctx + L.xcode);
   if (gx_lds_ok(g)) {

@@ -116,11 +116,11 @@ __device__ inline uint32_t bf16x2_of_bytes(uint32_t w, int sh) {
 
 template <int NBP>
 __device__ inline void stage_rows_bf16(const Geo& g, int WP, int RHx, const uint8_t* __restrict__ xc, int b,
-                                       int ih_first, uint8_t* patch) {
+                                       int ih_first, uint8_t* patch, int c0 = 0, int ncx = -1) {
   const int QW = g.W * NBP / 16;
-  const int n = g.C * RHx * QW;
+  const int n = (ncx < 0 ? g.C : ncx) * RHx * QW;
   const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
-  const uint4* src = reinterpret_cast<const uint4*>(xc) + (size_t)b * g.C * g.H * QW;
+  const uint4* src = reinterpret_cast<const uint4*>(xc) + ((size_t)b * g.C + c0) * g.H * QW;
   const int nt = blockDim.x;
   for (int base = threadIdx.x; base < n; base += 4 * nt) {
     uint4 v[4];
@@ -183,9 +183,11 @@ __device__ inline void tr4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, u
 // The int8 MFMA operand of one pixel (this lane's column / row l&15) for tile i:
 // xs[j][ks] byte e = slice j of the element at contraction index t = ks*64 + 16*(l>>4) + e.
 template <int NBP, int KS>
-__device__ inline void gather_xs(const uint8_t* patch, int rb, const int* ptab, int g4, v4i (&xs)[NBP][KS]) {
+__device__ inline void gather_xs(const uint8_t* patch, int rb, const int* ptab, int g4, v4i (&xs)[NBP][KS],
+                                 int ksn = KS) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
+    if (ks >= ksn) break;
     const int4* pt = reinterpret_cast<const int4*>(ptab + ks * 64 + 16 * g4);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -248,11 +250,27 @@ __device__ __noinline__ float code_literal(int p, int mode, float sw, float sa, 
 // forward: out[m, o] = sum_{i,j,k} ADC(ps_ijk[m, o]) * mask   (lsq.py:166-233)
 // block = 64-pixel m-tiles (grid-stride) x one 64-wide o-group; wave w = pixels 16w..16w+15.
 // ---------------------------------------------------------------------------------------
+// State words (what the backward needs of every partial sum, instead of the partial sum):
+// st[i][k][m/4][o][m%4], SB = 2 bytes for nba <= 5 else 4; for bit slice j, bit 3j = STE
+// pass (lsq.py:310-313), bit 3j+1 = ADC code != 0, bit 3j+2 = ADC code < 0 (lsq.py:321-332).
+template <int NBP>
+struct StWord;
+template <>
+struct StWord<4> { typedef uint16_t T; };
+template <>
+struct StWord<8> { typedef uint32_t T; };
+
+__device__ inline uint32_t st_bits(bool pass, float code) {
+  return (pass ? 1u : 0u) | ((code != 0.f) ? 2u : 0u) | ((code < 0.f) ? 4u : 0u);
+}
+
 template <int NBP, int KS>
 __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
-                                                         const float* __restrict__ sa_p, float* __restrict__ out) {
+                                                         const float* __restrict__ sa_p, float* __restrict__ out,
+                                                         uint8_t* __restrict__ st) {
+  typedef typename StWord<NBP>::T SW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int og = blockIdx.y;
   const int NOB = min(4, g.OB16);
@@ -264,13 +282,17 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   int* ptab = reinterpret_cast<int*>(cur); cur += (size_t)g.T * KS * 64 * 4;
   v4i* wfl = reinterpret_cast<v4i*>(cur); cur += (size_t)TT * g.nbw * NOB * KS * 1024;   // [tt][k][ob][ks][64]
   int4* prm = reinterpret_cast<int4*>(cur); cur += (size_t)TT * nkj * NOB * 16 * 16;    // [tt][j][k][NOB*16]
+  float* cfl = reinterpret_cast<float*>(cur); cur += (size_t)TT * nkj * NOB * 16 * 4;   // coef, same order
   float* ckl = reinterpret_cast<float*>(cur);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0) || g.mode != ADC_TERNARY;
+  const bool flag_lit = (pp.flags[0] != 0);
+  const bool literal = flag_lit || g.mode != ADC_TERNARY;
+  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
   const int Wo = 1 << v.lw;
+  const size_t MQ = (size_t)g.M >> 2;
 
   auto stage_tile = [&](int i, int tt) {
     batched_copy<4>(g.nbw * NOB * KS * 64, wfl + (size_t)tt * g.nbw * NOB * KS * 64, [&](int idx) -> v4i {
@@ -280,16 +302,21 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * 4 + ob) * WAVE + l];
       return w;
     });
-    if (!literal) {
+    if (!flag_lit) {
       batched_copy<2>(nkj * NOB * 16, prm + (size_t)tt * nkj * NOB * 16, [&](int idx) -> int4 {
         const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
         const int o = og * 64 + col;
         int4 p = make_int4(0, 0, 0, 0);
         if (o < g.Opad) {
           const int pi = pidx(g, i, j, k, o);
-          p = make_int4(pp.thi[pi], pp.tlo[pi], __float_as_int(pp.coef[pi]), 0);
+          p = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
         }
         return p;
+      });
+      batched_copy<4>(nkj * NOB * 16, cfl + (size_t)tt * nkj * NOB * 16, [&](int idx) -> float {
+        const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
+        const int o = og * 64 + col;
+        return (o < g.Opad) ? pp.coef[pidx(g, i, j, k, o)] : 0.f;
       });
     }
   };
@@ -322,39 +349,63 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
         __syncthreads();
       }
       const int tt = v.fwd_res ? i : 0;
+      const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;  // K-steps holding data in tile i
       v4i xs[NBP][KS];
-      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs);
+      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, ksn);
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
+      const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
       for (int k = 0; k < g.nbw; ++k) {
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
           if (ob < nob) {
+            const int o = (og * 4 + ob) * 16 + r16;
             v4i wk[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) wk[ks] = wt[((k * NOB + ob) * KS + ks) * 64 + lane];
+            uint32_t stw[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int j = 0; j < NBP; ++j) {
               if (j < g.nba) {
                 v4i ps = {0, 0, 0, 0};
 #pragma unroll
-                for (int ks = 0; ks < KS; ++ks) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps, 0, 0, 0);
+                for (int ks = 0; ks < KS; ++ks) if (ks < ksn) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps, 0, 0, 0);
+                const int pcol = (j * g.nbw + k) * NOB * 16 + ob * 16 + r16;
                 if (!literal) {
-                  const int4 pv = pt[(j * g.nbw + k) * NOB * 16 + ob * 16 + r16];
-                  const float cf = __int_as_float(pv.z);
+                  const int4 pv = pt[pcol];
+                  const float cf = ct[pcol];
 #pragma unroll
                   for (int r = 0; r < 4; ++r) {
-                    float a = (ps[r] >= pv.x) ? cf : 0.f;
-                    a = (ps[r] <= pv.y) ? -cf : a;
+                    const bool hi = ps[r] >= pv.x, lo = ps[r] <= pv.y;
+                    float a = hi ? cf : 0.f;
+                    a = lo ? -cf : a;
                     acc[ob][r] += a;
+                    const bool pass = (unsigned)(ps[r] - pv.z) <= (unsigned)pv.w;
+                    stw[r] |= ((pass ? 1u : 0u) | ((hi || lo) ? 2u : 0u) | (lo ? 4u : 0u)) << (3 * j);
                   }
                 } else {
-                  const int o = (og * 4 + ob) * 16 + r16;
                   const float al = pp.alpha[pidx(g, i, j, k, o)];
                   const float mk = ckl[k * g.nba + j];
+                  const int4 pv = pt[pcol];
 #pragma unroll
-                  for (int r = 0; r < 4; ++r) acc[ob][r] += adc_literal_sum(ps, g.mode, sw, sa, al, g.qn, g.qp, mk, r);
+                  for (int r = 0; r < 4; ++r) {
+                    acc[ob][r] += adc_literal_sum(ps, g.mode, sw, sa, al, g.qn, g.qp, mk, r);
+                    const bool pass = flag_lit ? (ste_literal(ps[r], g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f)
+                                               : ((unsigned)(ps[r] - pv.z) <= (unsigned)pv.w);
+                    const float code =
+                        has_code ? code_literal(ps[r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo) : 0.f;
+                    stw[r] |= st_bits(pass, code) << (3 * j);
+                  }
                 }
+              }
+            }
+            // state words of pixels wave*16 + 4*g4 + (0..3), channel o: one 4-pixel quad
+            if (o < g.O) {
+              const size_t q = ((size_t)(i * g.nbw + k) * MQ + (size_t)mt * 16 + wave * 4 + g4) * g.O + o;
+              if (sizeof(SW) == 2) {
+                reinterpret_cast<uint2*>(st)[q] = make_uint2(stw[0] | (stw[1] << 16), stw[2] | (stw[3] << 16));
+              } else {
+                reinterpret_cast<uint4*>(st)[q] = make_uint4(stw[0], stw[1], stw[2], stw[3]);
               }
             }
           }
@@ -377,7 +428,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 // grad_x (+ fused LSQ activation backward) as a transposed implicit GEMM: block = one band of
 // RI input rows of one image.  Per tile i and 32-wide kappa chunk:
 //   phase A  G_i[m, kappa] = g[m, o] * E_i[m, kappa],  E_i = sum_j cE_kj * STE_ijk[m, o]
-//            (ps recomputed on the int8 MFMA for every output pixel m touching the band),
+//            for every output pixel m touching the band, from the forward's state words,
 //            split into bf16 hi/mid/lo rows in LDS;
 //   phase B  gx[q, c] += sum_{kh,kw} sum_kappa G_i[m(q,kh,kw), kappa] * int8(w_k[(c,kh,kw), o])
 //            on bf16 MFMA, q = input position of the band, c = channel (lsq.py:257-317).
@@ -385,17 +436,18 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 // its output tiles in registers for the whole kernel, so there are no atomics; the LSQ
 // activation backward is applied in registers and gx stored once.
 // ---------------------------------------------------------------------------------------
-template <int NBP, int KS, int TPW, bool LSQ>
-__global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
-                                                            const v4i* __restrict__ wfrag,
+template <int NBP, int TPW, bool LSQ>
+__global__ __launch_bounds__(512, 2) void cim_bwd_gx_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
                                                             const uint4* __restrict__ wtc, Params pp,
                                                             const float* __restrict__ sw_p,
                                                             const float* __restrict__ sa_p,
                                                             const float* __restrict__ gout,
                                                             const float* __restrict__ x, float* __restrict__ gx,
                                                             float* __restrict__ gsa_part) {
+  typedef typename StWord<NBP>::T SW;
   // TPW: output tiles per wave (host guarantees NT <= 8 * TPW)
-  constexpr int GPB = 40;   // G / W row pitch in bf16: 32 kappa + 8 pad (bank spread, 16-B rows)
+  constexpr int GP = 32;    // G row pitch in bf16 (consecutive A-operand rows are contiguous)
+  constexpr int WPB = 40;   // W row pitch in bf16: 32 kappa + 8 pad (bank spread)
   constexpr int KX = 3;     // max kernel height / width (host guarantees KH, KW <= 3)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int nkj = g.nbw * g.nba;
@@ -407,47 +459,34 @@ __global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const u
   const int oh_hi = min(g.Ho - 1, (r1 - 1 + g.PH) / g.SH);
   const int nro = oh_hi - oh_lo + 1;
   const int npb = nro << v.lw;
-  const int RHb = (nro - 1) * g.SH + g.KH;
-  const int ih_first = oh_lo * g.SH - g.PH;
   const int Cp = v.CB * 16;
   const int ZROW = v.NPB;  // all-zero G row
+  const int PART = (v.NPB + 1) * GP;  // bf16 elements per split part
 
   uint8_t* cur = smem;
-  uint8_t* patch = cur; cur += al16((size_t)g.C * v.RHB * v.WP * NBP);
-  __bf16* Gs = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)3 * (v.NPB + 1) * GPB * 2);  // [part][row][GPB]
-  __bf16* Wb = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)g.KHW * Cp * GPB * 2);       // [khw][c][GPB]
-  v4i* wfl = reinterpret_cast<v4i*>(cur); cur += (size_t)g.NBLK * KS * 1024;                    // [kb][ks][64]
-  int2* msl = reinterpret_cast<int2*>(cur); cur += al16((size_t)nkj * g.Opad * 8);              // [j][k][Opad]
-  int* ptab = reinterpret_cast<int*>(cur); cur += KS * 64 * 4;
+  __bf16* Gs = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)3 * PART * 2);          // [part][row][GP]
+  __bf16* Wb = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)g.KHW * Cp * WPB * 2);   // [khw][c][WPB]
   float* ckl = reinterpret_cast<float*>(cur); cur += al16(3 * nkj * 4);
-  int* kbt = reinterpret_cast<int*>(cur); cur += al16((size_t)g.NBLK * 4);  // kb -> (k << 16) | o-block
   float* red = reinterpret_cast<float*>(cur);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0);
   const bool gvec = (g.O & 3) == 0;
-  const int PART = (v.NPB + 1) * GPB;  // bf16 elements per split part
+  const size_t MQ = (size_t)g.M >> 2;
+  const size_t m_band = (size_t)b * g.P + ((size_t)oh_lo << v.lw);  // first output pixel of the band
 
-  zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * RHb * v.WP * NBP / 4);
-  for (int t = threadIdx.x; t < 3 * GPB / 2; t += blockDim.x) {
-    const int part = t / (GPB / 2), w = t - part * (GPB / 2);
-    reinterpret_cast<uint32_t*>(Gs + part * PART + ZROW * GPB)[w] = 0u;
+  for (int t = threadIdx.x; t < 3 * GP / 2; t += blockDim.x) {
+    const int part = t / (GP / 2), w = t - part * (GP / 2);
+    reinterpret_cast<uint32_t*>(Gs + part * PART + ZROW * GP)[w] = 0u;
   }
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
-  for (int t = threadIdx.x; t < g.NBLK; t += blockDim.x) kbt[t] = ((t / g.OB16) << 16) | (t % g.OB16);
-  __syncthreads();
-  stage_rows<NBP>(g, v.WP, RHb, xcf, b, ih_first, patch);
 
-  // this wave's output tiles: t = wave + NW*u -> (q-block, c-block); per tile the G row of
-  // every tap for this lane's A-operand position q = qb*16 + r16, and x at the lane's four
-  // accumulator positions q = qb*16 + 4*g4 + r (channel cb*16 + r16)
+  // this wave's output tiles: t = wave + NW*u -> (q-block, c-block); the lane's A-operand
+  // position q = qb*16 + r16 and its four accumulator positions q = qb*16 + 4*g4 + r
   const int nq = nrow * g.W;
   const int QBb = (nq + 15) >> 4;
   const int NTb = QBb * v.CB;
-  // per tile: this lane's A-operand position relative to the band's first output row
-  // (ihp = ih + PH - oh_lo*SH, iwp = iw + PW; -1 when the position is padding)
   int ihp[TPW], iwp[TPW];
   float xpre[TPW][4];
   v4f acc[TPW];
@@ -467,22 +506,33 @@ __global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const u
       if (LSQ && t < NTb && qa < nq && c < g.C) xpre[u][r] = x[(((size_t)b * g.C + c) * g.H + r0) * g.W + qa];
     }
   }
+  // G row of every (tile, tap) for this lane's A-operand position (the zero row when the
+  // output pixel does not exist); in registers for two tiles per wave
+  constexpr int RIX = (TPW <= 2) ? TPW * KX * KX : 1;
+  int rowidx[RIX];
+  auto grow_of = [&](int u, int kh, int kw) -> int {
+    const int ohs = ihp[u] - kh, ows = iwp[u] - kw;
+    int row = ZROW;
+    if (ohs >= 0 && ows >= 0 && (ohs % g.SH) == 0 && (ows % g.SW) == 0) {
+      const int oh = ohs / g.SH, ow = ows / g.SW;
+      if (oh < nro && ow < g.Wo) row = (oh << v.lw) + ow;
+    }
+    return row;
+  };
+  if constexpr (TPW <= 2) {
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+      for (int kh = 0; kh < KX; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KX; ++kw) rowidx[(u * KX + kh) * KX + kw] = grow_of(u, kh, kw);
+  }
 
-  const int ngrp = (npb + 15) >> 4;
-  const float* gimg = gout + ((size_t)b * g.P + ((size_t)oh_lo << v.lw)) * g.O;
+  const int nquad = npb >> 2;          // 4-pixel quads of the band
+  const float invOB = 1.f / (float)g.OB16;
 
   for (int i = 0; i < g.T; ++i) {
     const int ci0 = (i * g.xbar) / g.KHW, ci1 = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
-    __syncthreads();
-    batched_copy<2>(g.NBLK * KS * 64, wfl, [&](int idx) -> v4i {
-      return wfrag[(size_t)i * KS * g.NBLK * 64 + ((idx >> 6) % KS) * g.NBLK * 64 + ((idx >> 6) / KS) * 64 + (idx & 63)];
-    });
-    if (!literal) {
-      const int npi = nkj * g.Opad;
-      batched_copy<2>(npi, msl, [&](int idx) -> int2 { return make_int2(pp.mlo[i * npi + idx], pp.mhi[i * npi + idx]); });
-    }
-    build_ptab(g, i, KS, RHb, v.WP, ptab);
-
     for (int kc = 0; kc < g.NKS; ++kc) {
       __syncthreads();
       // W rows of this tile and kappa chunk: Wb[khw][c][kappa] (zero for (c, khw) outside tile i)
@@ -502,7 +552,7 @@ __global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const u
               val[u] = make_uint4(0, 0, 0, 0);
               if (c < g.C && f >= i * g.xbar && f < min(g.K, (i + 1) * g.xbar))
                 val[u] = wtc[((size_t)row * g.NKS + kc) * 4 + q8];
-              dst[u] = row * (GPB / 8) + q8;
+              dst[u] = row * (WPB / 8) + q8;
             }
           }
 #pragma unroll
@@ -510,78 +560,91 @@ __global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const u
             if (dst[u] >= 0) reinterpret_cast<uint4*>(Wb)[dst[u]] = val[u];
         }
       }
-      // phase A: G rows of kappa blocks 2kc, 2kc+1 for every band output pixel
-      for (int u = wave; u < ngrp * 2; u += NW) {
-        const int grp = u >> 1, h2 = u & 1;
-        const int kb = 2 * kc + h2;
-        const int plr = grp * 16 + r16;
-        const bool pvalid = plr < npb;
-        const int pl = min(plr, npb - 1);
-        float G[4] = {0.f, 0.f, 0.f, 0.f};
+      // phase A: one item = 4 pixels x 4 consecutive kappa (same k, 4 channels)
+      for (int it = threadIdx.x; it < nquad * 8; it += blockDim.x) {
+        const int qd = it >> 3, kq = it & 7;
+        const int kb = 2 * kc + (kq >> 2);
+        float G[4][4];  // [pixel r][channel e]
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) G[r][e] = 0.f;
         if (kb < g.NBLK) {
-          const int kt = kbt[kb];
-          const int k = kt >> 16, ob0 = (kt & 0xFFFF) * 16 + 4 * g4;
-          float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (pvalid) {
-            const float* grow = gimg + (size_t)pl * g.O;
-            if (gvec && ob0 + 4 <= g.O) {
-              gv = *reinterpret_cast<const float4*>(grow + ob0);
+          const int k = fdiv(kb, g.OB16, invOB);
+          const int o0 = (kb - k * g.OB16) * 16 + (kq & 3) * 4;
+          const size_t m0 = m_band + 4 * (size_t)qd;
+          // state words of 4 pixels for channels o0..o0+3 (16 words, contiguous)
+          SW sv[4][4];
+          if (gvec && o0 + 4 <= g.O) {
+            const size_t q = ((size_t)(i * g.nbw + k) * MQ + (m0 >> 2)) * g.O + o0;
+            if (sizeof(SW) == 2) {
+              const uint4 a0 = reinterpret_cast<const uint4*>(st + q * 8)[0];
+              const uint4 a1 = reinterpret_cast<const uint4*>(st + q * 8)[1];
+              const uint32_t w8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sv[e][r] = (SW)(w8[2 * e + (r >> 1)] >> (16 * (r & 1)));
             } else {
-              if (ob0 + 0 < g.O) gv.x = grow[ob0 + 0];
-              if (ob0 + 1 < g.O) gv.y = grow[ob0 + 1];
-              if (ob0 + 2 < g.O) gv.z = grow[ob0 + 2];
-              if (ob0 + 3 < g.O) gv.w = grow[ob0 + 3];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint4 a = reinterpret_cast<const uint4*>(st)[q + e];
+                sv[e][0] = a.x; sv[e][1] = a.y; sv[e][2] = a.z; sv[e][3] = a.w;
+              }
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                sv[e][r] = 0;
+                if (o0 + e < g.O)
+                  sv[e][r] = reinterpret_cast<const SW*>(st)[(((size_t)(i * g.nbw + k) * MQ + (m0 >> 2)) * g.O + o0 + e) * 4 + r];
+              }
+          }
+          float gv[4][4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float* grow = gout + (m0 + r) * g.O;
+            if (gvec && o0 + 4 <= g.O) {
+              const float4 t4 = *reinterpret_cast<const float4*>(grow + o0);
+              gv[r][0] = t4.x; gv[r][1] = t4.y; gv[r][2] = t4.z; gv[r][3] = t4.w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) gv[r][e] = (o0 + e < g.O) ? grow[o0 + e] : 0.f;
             }
           }
-          const int rb = ((pl >> v.lw) * g.SH) * v.WP + (pl & ((1 << v.lw) - 1)) * g.SW;
-          v4i xs[NBP][KS];
-          gather_xs<NBP, KS>(patch, rb, ptab, g4, xs);
-          v4i wk[KS];
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) wk[ks] = wfl[(kb * KS + ks) * 64 + lane];
-          float E[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int j = 0; j < NBP; ++j) {
             if (j < g.nba) {
-              v4i ps = {0, 0, 0, 0};
-#pragma unroll
-              for (int ks = 0; ks < KS; ++ks) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(wk[ks], xs[j][ks], ps, 0, 0, 0);
               const float ce = ckl[nkj + k * g.nba + j];
-              if (!literal) {
-                const int4* ms = reinterpret_cast<const int4*>(msl + (j * g.nbw + k) * g.Opad + ob0);
-                const int4 m01 = ms[0], m23 = ms[1];
-                E[0] += ((unsigned)(ps[0] - m01.x) <= (unsigned)m01.y) ? ce : 0.f;
-                E[1] += ((unsigned)(ps[1] - m01.z) <= (unsigned)m01.w) ? ce : 0.f;
-                E[2] += ((unsigned)(ps[2] - m23.x) <= (unsigned)m23.y) ? ce : 0.f;
-                E[3] += ((unsigned)(ps[3] - m23.z) <= (unsigned)m23.w) ? ce : 0.f;
-              } else {
-                const int pi = pidx(g, i, j, k, ob0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  E[r] += ste_literal(ps[r], g.mode, sw, sa, pp.alpha[pi + r], g.thr_hi, g.thr_lo) * ce;
-              }
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) G[r][e] += ((sv[e][r] >> (3 * j)) & 1u) ? ce : 0.f;
             }
           }
-          G[0] = gv.x * E[0];
-          G[1] = gv.y * E[1];
-          G[2] = gv.z * E[2];
-          G[3] = gv.w * E[3];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) G[r][e] *= gv[r][e];
         }
-        if (pvalid) {
-          // lane holds kappa (chunk-local) h2*16 + 4*g4 + r of pixel pl: 4 consecutive bf16 per part
+        // rows 4*qd + r, chunk-local kappa kq*4 .. +4: three bf16 parts
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
           uint32_t ph[2], pm[2], pl2[2];
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            float a0 = G[2 * e], a1 = G[2 * e + 1];
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const float a0 = G[r][2 * e2], a1 = G[r][2 * e2 + 1];
             const __bf16 h0 = (__bf16)a0, h1 = (__bf16)a1;
             const float s0 = a0 - (float)h0, s1 = a1 - (float)h1;
-            const __bf16 m0 = (__bf16)s0, m1 = (__bf16)s1;
-            const __bf16 l0 = (__bf16)(s0 - (float)m0), l1 = (__bf16)(s1 - (float)m1);
-            ph[e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-            pm[e] = (uint32_t)__builtin_bit_cast(uint16_t, m0) | ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
-            pl2[e] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            const __bf16 m0b = (__bf16)s0, m1b = (__bf16)s1;
+            const __bf16 l0 = (__bf16)(s0 - (float)m0b), l1 = (__bf16)(s1 - (float)m1b);
+            ph[e2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            pm[e2] = (uint32_t)__builtin_bit_cast(uint16_t, m0b) | ((uint32_t)__builtin_bit_cast(uint16_t, m1b) << 16);
+            pl2[e2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
           }
-          const int off = plr * GPB + h2 * 16 + 4 * g4;
+          const int off = (4 * qd + r) * GP + kq * 4;
           *reinterpret_cast<uint2*>(Gs + off) = make_uint2(ph[0], ph[1]);
           *reinterpret_cast<uint2*>(Gs + PART + off) = make_uint2(pm[0], pm[1]);
           *reinterpret_cast<uint2*>(Gs + 2 * PART + off) = make_uint2(pl2[0], pl2[1]);
@@ -600,18 +663,14 @@ __global__ __launch_bounds__(512) void cim_bwd_gx_v4_kernel(Geo g, V3 v, const u
 #pragma unroll
             for (int kw = 0; kw < KX; ++kw) {
               if (kh < g.KH && kw < g.KW) {
-                // G row of output pixel m(q, kh, kw): the all-zero row when it does not exist
-                const int ohs = ihp[u] - kh, ows = iwp[u] - kw;
-                int row = ZROW;
-                if (ohs >= 0 && ows >= 0 && (ohs % g.SH) == 0 && (ows % g.SW) == 0) {
-                  const int oh = ohs / g.SH, ow = ows / g.SW;
-                  if (oh < nro && ow < g.Wo) row = (oh << v.lw) + ow;
-                }
+                int row;
+                if constexpr (TPW <= 2) row = rowidx[(u * KX + kh) * KX + kw];
+                else row = grow_of(u, kh, kw);
                 const int khw = kh * g.KW + kw;
-                const v8bf gh = *reinterpret_cast<const v8bf*>(Gs + row * GPB + 8 * g4);
-                const v8bf gm = *reinterpret_cast<const v8bf*>(Gs + PART + row * GPB + 8 * g4);
-                const v8bf gl = *reinterpret_cast<const v8bf*>(Gs + 2 * PART + row * GPB + 8 * g4);
-                const v8bf wv = *reinterpret_cast<const v8bf*>(Wb + (khw * Cp + cb * 16 + r16) * GPB + 8 * g4);
+                const v8bf gh = *reinterpret_cast<const v8bf*>(Gs + row * GP + 8 * g4);
+                const v8bf gm = *reinterpret_cast<const v8bf*>(Gs + PART + row * GP + 8 * g4);
+                const v8bf gl = *reinterpret_cast<const v8bf*>(Gs + 2 * PART + row * GP + 8 * g4);
+                const v8bf wv = *reinterpret_cast<const v8bf*>(Wb + (khw * Cp + cb * 16 + r16) * WPB + 8 * g4);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, wv, a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm, wv, a, 0, 0, 0);
                 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, wv, a, 0, 0, 0);
@@ -742,6 +801,8 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
   const int NOB = min(2, g.OB16);
   const int nob = min(2, g.OB16 - og * 2);
   const int c0 = (i * g.xbar) / g.KHW;
+  const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;
+  const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;  // f-blocks holding data in tile i
   const int ncx = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW - c0 + 1;
   const size_t pf = al16((size_t)v.NCG * v.RH * v.WP * NBP);
   const size_t pbsz = INIT ? 0 : al16((size_t)v.NCG * v.RH * v.WP * NBP * 2);
@@ -843,7 +904,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
     load_gv(m0 + 64, gnext);
 
     v4i xs[NBP][KS];
-    gather_xs<NBP, KS>(patch, rb, ptab, g4, xs);
+    gather_xs<NBP, KS>(patch, rb, ptab, g4, xs, ksn);
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob) {
       if (ob < nob) {
@@ -863,7 +924,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
             if (j < g.nba) {
               v4i ps = {0, 0, 0, 0};
 #pragma unroll
-              for (int ks = 0; ks < KS; ++ks) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps, 0, 0, 0);
+              for (int ks = 0; ks < KS; ++ks) if (ks < ksn) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps, 0, 0, 0);
               const int kj = k * g.nba + j;
               float qs = 0.f;
               if (INIT) {
@@ -894,15 +955,24 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
                   }
                 }
               }
+#ifdef CIMQ_EXP_GW_NOQ
+              if (qs == 1234.5f) qacc[kj * 32 + ocol] = qs;
+#else
               if (INIT || has_code) {
                 qs += __shfl_xor(qs, 16);
                 qs += __shfl_xor(qs, 32);
                 if (g4 == 0) atomicAdd(&qacc[kj * 32 + ocol], qs);
               }
+#endif
             }
           }
         }
+#ifdef CIMQ_EXP_GW_NOGEMM
+        if (!INIT) gwa[0][ob][0] += D[0][0] + D[NBP - 1][3];
+        if (false) {
+#else
         if (!INIT) {
+#endif
           // B operands (k = (j-pair half h2, pixel r)) for every j-pair, then the f-blocks
           constexpr int NS = NBP / 2;
           v8bf bh[NS], bm[NS], bl[NS];
@@ -919,7 +989,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
           const uint32_t* pB = reinterpret_cast<const uint32_t*>(patchB);
 #pragma unroll
           for (int fb = 0; fb < FBX; ++fb) {
-            if (fb < g.FBT) {
+            if (fb < fbn) {
               v4f accw = gwa[fb][ob];
 #pragma unroll
               for (int s2 = 0; s2 < NS; ++s2) {
@@ -971,6 +1041,238 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
     const int fl = t >> 5, col = t & 31;
     const int o = og * 32 + col;
     if (o < g.Opad) gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o] = gwacc[t];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// grad_w from the forward's state words: block = (pixel chunk, tile i, 32 output channels);
+//   D_j[m, o] = sum_k cD_kj * STE_ijk[m, o]
+//   gw_i[f, o] += sum_{j, m} xhat_j[m, f] * (g[m, o] * D_j[m, o])     (bf16x3 MFMA)
+// Only the input channels of tile i are staged (as bf16 backward slices); grad_out and the
+// state words are read straight from memory, one pixel tile ahead.
+// ---------------------------------------------------------------------------------------
+template <int NBP, int FBX, int NBWX>
+__global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
+                                                               const uint8_t* __restrict__ xcb, Params pp,
+                                                               const float* __restrict__ gout, int rows_per_chunk,
+                                                               float* __restrict__ gw_slab) {
+  constexpr int NS = NBP / 2;
+  constexpr int SWD = NBP / 2;  // state dwords per (pixel quad, channel): 4 x uint16 or 4 x uint32
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int nkj = g.nbw * g.nba;
+  const int i = blockIdx.y, ob = blockIdx.z;  // one 16-channel block
+  const int c0 = (i * g.xbar) / g.KHW;
+  const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;  // f-blocks holding data in tile i
+  const int ncx = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW - c0 + 1;
+  const size_t pbsz = al16((size_t)v.NCG * v.RH * v.WP * NBP * 2);
+  const size_t gwsz = (size_t)g.FBT * 16 * 16 * 4;
+
+  uint8_t* cur = smem;
+  uint8_t* patchB = cur;
+  float* gwacc = reinterpret_cast<float*>(cur);  // aliases the patch after the pixel loop
+  cur += max(pbsz, gwsz);
+  int* ptab = reinterpret_cast<int*>(cur); cur += 128 * 4;
+  float* ckl = reinterpret_cast<float*>(cur);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int mbeg = blockIdx.x * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
+  const int Wo = 1 << v.lw;
+  const size_t MQ = (size_t)g.M >> 2;
+  const int o = ob * 16 + r16;
+  const bool ocol = o < g.O;
+
+  for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
+  build_ptab(g, i, 2, v.RH, v.WP, ptab, c0);
+  zero_lds(reinterpret_cast<uint32_t*>(patchB), (int)(pbsz / 4));
+  __syncthreads();
+
+  // this lane's 4 accumulator-row pixels (B-operand k-values) and its f-row per f-block
+  int rb4[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = wave * 16 + 4 * g4 + r;
+    rb4[r] = ((q >> v.lw) * g.SH) * v.WP + (q & (Wo - 1)) * g.SW;
+  }
+  int ptf[FBX];
+#pragma unroll
+  for (int fb = 0; fb < FBX; ++fb) ptf[fb] = (fb < g.FBT) ? ptab[fb * 16 + r16] : 0;
+
+  // grad_out and raw state dwords of this lane's 4 pixels, channel o
+  auto load_in = [&](int m0, float (&gd)[4], uint32_t (&sd)[NBWX][SWD]) {
+    const bool ok = m0 < mend && ocol;
+    const size_t mq = ((size_t)m0 >> 2) + wave * 4 + g4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gd[r] = ok ? gout[(size_t)(m0 + wave * 16 + 4 * g4 + r) * g.O + o] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NBWX; ++k) {
+#pragma unroll
+      for (int d = 0; d < SWD; ++d) sd[k][d] = 0u;
+      if (k < g.nbw && ok) {
+        const size_t q = ((size_t)(i * g.nbw + k) * MQ + mq) * g.O + o;
+        if (SWD == 2) {
+          const uint2 w = reinterpret_cast<const uint2*>(st)[q];
+          sd[k][0] = w.x; sd[k][1] = w.y;
+        } else {
+          const uint4 w = reinterpret_cast<const uint4*>(st)[q];
+          sd[k][0] = w.x; sd[k][1] = w.y;
+          if (SWD == 4) { sd[k][SWD - 2] = w.z; sd[k][SWD - 1] = w.w; }
+        }
+      }
+    }
+  };
+  auto word = [&](const uint32_t (&sd)[NBWX][SWD], int k, int r) -> uint32_t {
+    if (SWD == 2) return (sd[k][r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
+    return sd[k][r];
+  };
+  float gnext[4];
+  uint32_t snext[NBWX][SWD];
+  load_in(mbeg, gnext, snext);
+
+  v4f gwa[FBX];
+#pragma unroll
+  for (int a = 0; a < FBX; ++a) gwa[a] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int tiles_per_img = g.P >> 6;
+
+  for (int m0 = mbeg; m0 < mend; m0 += 64) {
+    const int mt = m0 >> 6;
+    const int b = mt / tiles_per_img, p0 = (mt - b * tiles_per_img) * 64;
+    const int ih_first = (p0 >> v.lw) * g.SH - g.PH;
+    __syncthreads();
+    stage_rows_bf16<NBP>(g, v.WP, v.RH, xcb, b, ih_first, patchB, c0, ncx);
+    float gcur[4];
+    uint32_t scur[NBWX][SWD];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gcur[r] = gnext[r];
+#pragma unroll
+    for (int k = 0; k < NBWX; ++k)
+#pragma unroll
+      for (int d = 0; d < SWD; ++d) scur[k][d] = snext[k][d];
+    __syncthreads();
+    load_in(m0 + 64, gnext, snext);
+
+    float D[NBP][4];
+#pragma unroll
+    for (int j = 0; j < NBP; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) D[j][r] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NBWX; ++k) {
+      if (k < g.nbw) {
+#pragma unroll
+        for (int j = 0; j < NBP; ++j) {
+          if (j < g.nba) {
+            const float cd = ckl[2 * nkj + k * g.nba + j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) D[j][r] += ((word(scur, k, r) >> (3 * j)) & 1u) ? cd : 0.f;
+          }
+        }
+      }
+    }
+    // B operands (k = (j-pair half h2, pixel r)) for every j-pair, then the f-blocks
+    v8bf bh[NS], bm[NS], bl[NS];
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) {
+      float ev[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = 2 * s2 + (e >> 2), r = e & 3;
+        ev[e] = (j < g.nba) ? gcur[r] * D[j][r] : 0.f;
+      }
+      split3x8(ev, bh[s2], bm[s2], bl[s2]);
+    }
+    const uint32_t* pB = reinterpret_cast<const uint32_t*>(patchB);
+#pragma unroll
+    for (int fb = 0; fb < FBX; ++fb) {
+      if (fb < fbn) {
+        v4f accw = gwa[fb];
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) {
+          if (2 * s2 < g.nba) {
+            uint32_t d[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d[r] = pB[(rb4[r] + ptf[fb]) * NS + s2];
+            v4i a;
+            a[0] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x05040100u);
+            a[1] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x05040100u);
+            a[2] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
+            a[3] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
+            const v8bf xa = as_v8bf(a);
+            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bh[s2], accw, 0, 0, 0);
+            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bm[s2], accw, 0, 0, 0);
+            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bl[s2], accw, 0, 0, 0);
+          }
+        }
+        gwa[fb] = accw;
+      }
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < g.FBT * 16 * 16; t += blockDim.x) gwacc[t] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int fb = 0; fb < FBX; ++fb)
+    if (fb < g.FBT)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * 16 + r16], gwa[fb][r]);
+  __syncthreads();
+  const int mc = blockIdx.x;
+  for (int t = threadIdx.x; t < g.FBT * 16 * 16; t += blockDim.x) {
+    const int fl = t >> 4, col = t & 15;
+    const int oo = ob * 16 + col;
+    gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + oo] = gwacc[t];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// grad_alpha_cim partial sums from the state words: ga[i, k, j, o] = sum_m code_ijk[m, o] *
+// g[m, o] (lsq.py:321-333).  Block = (pixel chunk, (i, k)); thread = one channel o (O | 256)
+// and a strided run of 4-pixel quads; per-(o, j) sums meet in LDS once.
+// ---------------------------------------------------------------------------------------
+template <int NBP>
+__global__ __launch_bounds__(256) void cim_galpha_v5_kernel(Geo g, const uint8_t* __restrict__ st,
+                                                            const float* __restrict__ gout, int rows_per_chunk,
+                                                            float* __restrict__ ga_slab) {
+  typedef typename StWord<NBP>::T SW;
+  __shared__ float red[256 * 8];
+  const int ik = blockIdx.y, i = ik / g.nbw, k = ik - i * g.nbw;
+  const int nkj = g.nbw * g.nba;
+  const int o = threadIdx.x % g.O, qs0 = threadIdx.x / g.O, qstep = blockDim.x / g.O;
+  const size_t MQ = (size_t)g.M >> 2;
+  const int mb = (int)blockIdx.x * rows_per_chunk;
+  const int q0 = mb >> 2, q1 = min(mb + rows_per_chunk, g.M) >> 2;
+  float acc[NBP];
+#pragma unroll
+  for (int j = 0; j < NBP; ++j) acc[j] = 0.f;
+  for (int q = q0 + qs0; q < q1; q += qstep) {
+    const size_t e = ((size_t)ik * MQ + q) * g.O + o;
+    SW sv[4];
+    if (sizeof(SW) == 2) {
+      const uint2 w = reinterpret_cast<const uint2*>(st)[e];
+      sv[0] = (SW)w.x; sv[1] = (SW)(w.x >> 16); sv[2] = (SW)w.y; sv[3] = (SW)(w.y >> 16);
+    } else {
+      const uint4 w = reinterpret_cast<const uint4*>(st)[e];
+      sv[0] = w.x; sv[1] = w.y; sv[2] = w.z; sv[3] = w.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float gv = gout[((size_t)q * 4 + r) * g.O + o];
+#pragma unroll
+      for (int j = 0; j < NBP; ++j) {
+        const uint32_t bits = sv[r] >> (3 * j);
+        const float c = (bits & 2u) ? ((bits & 4u) ? -gv : gv) : 0.f;
+        acc[j] += c;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NBP; ++j) red[j * 256 + threadIdx.x] = acc[j];
+  __syncthreads();
+  for (int t = threadIdx.x; t < g.O * g.nba; t += blockDim.x) {
+    const int j = t / g.O, oo = t - j * g.O;
+    float sacc = 0.f;
+    for (int s2 = 0; s2 < qstep; ++s2) sacc += red[j * 256 + s2 * g.O + oo];
+    ga_slab[(((size_t)blockIdx.x * g.T + i) * nkj + k * g.nba + j) * g.Opad + oo] = sacc;
   }
 }
 

@@ -50,9 +50,11 @@ def _desc(**kw):
 def test_query_sizes_resnet20_s1(lib):
     s = L.query_sizes(_desc())
     # ctx holds the packed forward slice word and the backward slice word (4 bytes each for
-    # nba <= 4) per input element, plus small weight/param tables
+    # nba <= 4) per input element, a 2-byte state word per partial-sum (tile, w-slice, pixel,
+    # channel), plus small weight/param tables
     nin = 256 * 16 * 32 * 32
-    assert 8 * nin <= s.ctx_bytes < 8 * nin + (1 << 20)
+    nst = 2 * 3 * (256 * 32 * 32) * 16 * 2  # T=2 tiles, nbw=3, M pixels, O=16, uint16
+    assert 8 * nin + nst <= s.ctx_bytes < 8 * nin + nst + (1 << 20)
     assert s.bwd_workspace_bytes > 0
 
 

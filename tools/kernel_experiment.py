@@ -41,8 +41,10 @@ def do_time(layer, iters):
     import torch
     import bench
     from cim_quantization_amd import _lib
-    names = [r[0] for r in bench.RESNET20]
-    bench.RESNET20[:] = [bench.RESNET20[names.index(layer)]]
+    if not hasattr(bench, "_ALL_LAYERS"):
+        bench._ALL_LAYERS = list(bench.RESNET20)
+    names = [r[0] for r in bench._ALL_LAYERS]
+    bench.RESNET20[:] = [bench._ALL_LAYERS[names.index(layer)]]
     layers, xs, gs = bench.build(torch.device("cuda:0"), 256)
     m, x, g = layers[0], xs[0], gs[0]
     for name in VARIANTS:
