@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -25,6 +25,8 @@ EXPORTED_SYMBOLS = (
     "cimq_query_sizes",
     "cimq_forward",
     "cimq_backward",
+    "cimq_module_forward",
+    "cimq_module_backward",
     "cimq_alpha_init",
     "cimq_debug_partial_sums",
     "cimq_profile_start",
@@ -54,6 +56,13 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class LsqDesc(ctypes.Structure):
+    """Mirror of ``cimq_lsq_desc``."""
+
+    _fields_ = [("qn_w", ctypes.c_float), ("qp_w", ctypes.c_float), ("gscale_a", ctypes.c_float),
+                ("gscale_w", ctypes.c_float), ("nbits_alpha", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+
+
 class Sizes(ctypes.Structure):
     """Mirror of ``cimq_sizes``."""
 
@@ -81,6 +90,10 @@ def _bind(lib):
     lib.cimq_forward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 11
     lib.cimq_backward.restype = ctypes.c_int
     lib.cimq_backward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 14
+    lib.cimq_module_forward.restype = ctypes.c_int
+    lib.cimq_module_forward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 11
+    lib.cimq_module_backward.restype = ctypes.c_int
+    lib.cimq_module_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 16
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
     lib.cimq_debug_partial_sums.restype = ctypes.c_int
@@ -133,6 +146,14 @@ def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w
     d.input_kind = int(input_kind)
     d.lsq_qp = float(lsq_qp)
     return d
+
+
+def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha) -> LsqDesc:
+    q = LsqDesc()
+    q.qn_w, q.qp_w = float(qn_w), float(qp_w)
+    q.gscale_a, q.gscale_w = float(gscale_a), float(gscale_w)
+    q.nbits_alpha = int(nbits_alpha)
+    return q
 
 
 def query_sizes(desc: ConvDesc) -> Sizes:

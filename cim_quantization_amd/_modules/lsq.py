@@ -17,7 +17,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from ..functional import alpha_cim_init, cim_conv2d_lsq, get_cim_output_signed  # noqa: F401
+from ..functional import alpha_cim_init, cim_conv2d_lsq, cim_module_conv, get_cim_output_signed  # noqa: F401
 from ._quan_base import (_ActQ, _Conv2dQ, _Conv2dQCiM, _LinearQ, Qmodes, grad_scale,  # noqa: F401
                          round_pass)
 
@@ -49,6 +49,7 @@ class Conv2dLSQCiM(_Conv2dQCiM):
                          nbits_w=nbits_w, nbits_a=nbits_a, nbits_alpha=nbits_alpha, wbitslice=wbitslice,
                          abitslice=abitslice, xbar=xbar, adcbits=adcbits, stochastic_quant=stochastic_quant)
         self._state_cache = None  # host mirror of (init_state, init_state_cim) to avoid a sync per step
+        self.fused = True  # steady state through cimq_module_forward/backward (False: torch quantisers)
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
@@ -74,6 +75,16 @@ class Conv2dLSQCiM(_Conv2dQCiM):
             flags[0] = True
         if self.binary_mask.device != x.device:
             self.binary_mask = self.binary_mask.to(x.device)
+        if (self.fused and flags[0] and (flags[1] or self.alpha_cim is None) and self.adcbits != 0
+                and not self.stochastic_quant):
+            # steady state: the three quantisers and the CiM conv in one library call each way
+            out = cim_module_conv(x, self.weight, self.alpha_act, self.alpha_weight, self.alpha_cim,
+                                  self.binary_mask, self.signed_act, self.stride, self.padding, self.dilation,
+                                  self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
+                                  self.xbar, self.nbits_alpha)
+            if self.bias is not None:
+                out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
+            return out
         sa = grad_scale(self.alpha_act, 1.0 / math.sqrt(x.numel() * qp_a))            # lsq.py:547-548
         sw = grad_scale(self.alpha_weight, 1.0 / math.sqrt(self.weight.numel() * qp_w))  # lsq.py:553-554
         w_q = round_pass((self.weight / sw).clamp(qn_w, qp_w)) * sw                   # lsq.py:555

@@ -12,6 +12,7 @@
 
 #include "../../include/cimq.h"
 #include "cimq_kernels_v3.hip"
+#include "cimq_lsq.hip"
 
 using namespace cimq;
 
@@ -106,7 +107,9 @@ int make_geo(const cimq_conv_desc* d, Geo* out) {
 }
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st, total;
+  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st;
+  size_t lsq_scal, lsq_wq, lsq_aq;  // module entry points: sa/sw/alpha scale, w_q, alpha_q
+  size_t total;
 };
 
 CtxLayout ctx_layout(const Geo& g) {
@@ -128,6 +131,9 @@ CtxLayout ctx_layout(const Geo& g) {
   L.flags = o; o = align256(o + 16);
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   L.st = o; o = align256(o + (size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4));
+  L.lsq_scal = o; o = align256(o + 16 * 4);
+  L.lsq_wq = o; o = align256(o + (size_t)g.O * g.K * 4);
+  L.lsq_aq = o; o = align256(o + npar * 4);
   L.total = o;
   return L;
 }
@@ -171,7 +177,7 @@ const size_t kLdsMax = 160 * 1024;
 bool gx_lds_ok(const Geo& g) { return lds_tile(g) + sizeof(float) * g.C * g.HW <= kLdsMax - 1024; }
 
 struct WsLayout {
-  size_t gw_slab, ga_slab, lsq_part, total;
+  size_t gw_slab, ga_slab, lsq_part, gaq, wpart, bpo, total;
   int rows, nchunks;
 };
 
@@ -182,6 +188,11 @@ WsLayout ws_layout(const Geo& g) {
   W.gw_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.FBT * 16 * g.Opad);
   W.ga_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.nbw * g.nba * g.Opad);
   W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * ((g.H + 7) / 8)));
+  // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
+  // a [B, P, O] staging copy of out / grad_out for the general kernels
+  W.gaq = o; o = align256(o + sizeof(float) * (size_t)g.T * g.nbw * g.nba * g.O);
+  W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
+  W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
   W.total = o;
   return W;
 }
@@ -622,6 +633,132 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
     CIMQ_TRY(check_hip("sum_partials"));
   }
   return CIMQ_OK;
+}
+
+static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
+  if (!q) return fail(CIMQ_EINVAL, "null LSQ descriptor");
+  if (!(q->qn_w < q->qp_w) || !(q->gscale_a > 0.f) || !(q->gscale_w > 0.f))
+    return fail(CIMQ_EINVAL, "bad LSQ descriptor");
+  if (q->nbits_alpha < 0 || q->nbits_alpha > 16 || q->nbits_alpha == 1)
+    return fail(CIMQ_EINVAL, "nbits_alpha must be 0 (no alpha_cim) or 2..16");
+  a->qn_w = q->qn_w;
+  a->qp_w = q->qp_w;
+  a->gs_a = q->gscale_a;
+  a->gs_w = q->gscale_w;
+  a->nbits_alpha = q->nbits_alpha;
+  a->nalpha = g.T * g.nbw * g.nba * g.O;
+  return CIMQ_OK;
+}
+
+int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                        const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                        const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
+                        void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  LsqArgs la;
+  CIMQ_TRY(lsq_args(g, q, &la));
+  if (!x || !weight || !alpha_act || !alpha_weight || !binary_mask || !signed_act || !out || !ctx || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
+  if (has_alpha && (!alpha_cim || la.nbits_alpha == 0)) return fail(CIMQ_EINVAL, "adc 1 / 1.5 need alpha_cim");
+  if (!has_alpha) la.nbits_alpha = 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
+  CtxLayout L = ctx_layout(g);
+  float* scal = reinterpret_cast<float*>(c + L.lsq_scal);
+  float* wq = reinterpret_cast<float*>(c + L.lsq_wq);
+  float* aq = reinterpret_cast<float*>(c + L.lsq_aq);
+  hipLaunchKernelGGL(prep_lsq_kernel, dim3(1), dim3(1024), 0, s, g, la, alpha_act, alpha_weight, weight,
+                     alpha_cim, scal, wq, aq);
+  CIMQ_TRY(check_hip("prep_lsq"));
+  CIMQ_TRY(prep_all(g, x, wq, scal, scal + 1, has_alpha ? aq : nullptr, binary_mask, signed_act, c, s, true, true));
+  const Plan3 p = v3_plan(g);
+  if (p.ok) {
+    g.onchw = 1;
+    if (g.NBP == 4) return launch_fwd<4, false>(g, c, scal + 1, scal, out, nullptr, nullptr, s);
+    return launch_fwd<8, false>(g, c, scal + 1, scal, out, nullptr, nullptr, s);
+  }
+  // general kernels write [B, P, O]; the module returns NCHW
+  WsLayout W = ws_layout(g);
+  float* bpo = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + W.bpo);
+  if (g.NBP == 4) CIMQ_TRY((launch_fwd<4, false>(g, c, scal + 1, scal, bpo, nullptr, nullptr, s)));
+  else CIMQ_TRY((launch_fwd<8, false>(g, c, scal + 1, scal, bpo, nullptr, nullptr, s)));
+  hipLaunchKernelGGL(bpo_to_nchw_kernel, dim3(std::min(cdiv((long long)g.M * g.O, 256), 8192)), dim3(256), 0, s,
+                     g, bpo, out);
+  return check_hip("bpo_to_nchw");
+}
+
+int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out, const float* x,
+                         const float* weight, const float* alpha_act, const float* alpha_weight,
+                         const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,
+                         const void* ctx, float* grad_x, float* grad_weight, float* grad_alpha_act,
+                         float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  LsqArgs la;
+  CIMQ_TRY(lsq_args(g, q, &la));
+  (void)alpha_act; (void)alpha_weight; (void)binary_mask;
+  if (!grad_out || !x || !weight || !signed_act || !ctx || !grad_x || !grad_weight || !grad_alpha_act ||
+      !grad_alpha_weight || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
+  if (has_alpha && (!alpha_cim || !grad_alpha_cim || la.nbits_alpha == 0))
+    return fail(CIMQ_EINVAL, "adc 1 / 1.5 need alpha_cim and grad_alpha_cim");
+  if (!has_alpha) la.nbits_alpha = 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  const float* scal = reinterpret_cast<const float*>(c + L.lsq_scal);
+  const float* sa = scal;
+  const float* sw = scal + 1;
+  const Plan3 p = v3_plan(g);
+  const float* gsrc = grad_out;
+  if (p.ok) {
+    g.onchw = 1;
+  } else {
+    float* bpo = reinterpret_cast<float*>(w + W.bpo);
+    hipLaunchKernelGGL(nchw_to_bpo_kernel, dim3(std::min(cdiv((long long)g.M * g.O, 256), 8192)), dim3(256), 0, s,
+                       g, grad_out, bpo);
+    CIMQ_TRY(check_hip("nchw_to_bpo"));
+    gsrc = bpo;
+  }
+  bool lsq_fused = false;
+  if (g.NBP == 4) CIMQ_TRY(dispatch_bwd<4>(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused));
+  else CIMQ_TRY(dispatch_bwd<8>(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused));
+  // grad_w fused with the weight quantiser's backward
+  const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
+  const int nwb = cdiv(nout, 64);
+  float* wpart = reinterpret_cast<float*>(w + W.wpart);
+  hipLaunchKernelGGL(reduce_gw_lsq_kernel, dim3(nwb), dim3(256), 0, s, g, la, W.nchunks,
+                     reinterpret_cast<const float*>(w + W.gw_slab), scal, weight, grad_weight, wpart);
+  CIMQ_TRY(check_hip("reduce_gw_lsq"));
+  if (has_alpha) {
+    const double numel = (double)g.B * g.T * g.nbw * g.nba * g.P * g.O;
+    const float cgrad = (float)(1.0 / sqrt(numel * (double)g.qp));  // lsq.py:323,330
+    float* gaq = reinterpret_cast<float*>(w + W.gaq);
+    CIMQ_TRY(launch_reduce_galpha(g, c, w, cgrad, 0, sw, sa, gaq, s));
+    hipLaunchKernelGGL(alpha_cim_bwd_kernel, dim3(1), dim3(1024), 0, s, la, alpha_cim, scal, gaq, grad_alpha_cim);
+    CIMQ_TRY(check_hip("alpha_cim_bwd"));
+  }
+  float* part = reinterpret_cast<float*>(w + W.lsq_part);
+  int nparts;
+  if (lsq_fused) {
+    nparts = g.B * p.v.nbands;
+  } else {
+    int grid = cdiv(g.Nin, 256);
+    if (grid > kLsqParts) grid = kLsqParts;
+    hipLaunchKernelGGL(lsq_act_bwd_kernel, dim3(grid), dim3(256), 0, s, g.Nin, x, sa, g.lsq_qp, grad_x, part);
+    CIMQ_TRY(check_hip("lsq_act_bwd"));
+    nparts = grid;
+  }
+  hipLaunchKernelGGL(lsq_scalars_finish_kernel, dim3(1), dim3(1024), 0, s, la, nwb, wpart, nparts, part,
+                     grad_alpha_weight, grad_alpha_act);
+  return check_hip("lsq_scalars_finish");
 }
 
 int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,

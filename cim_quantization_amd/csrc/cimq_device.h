@@ -28,6 +28,7 @@ struct Geo {
   float lsq_qp;
   int psmax;               // bound on |partial sum| used by the threshold search
   long long Nin;           // B*C*H*W
+  int onchw;               // out / grad_out layout: 0 = [B, P, O] (the Function's), 1 = NCHW (the module's)
 };
 
 // Per-(tile i, a-slice j, w-slice k, out-channel o) ADC / STE parameters, SoA.

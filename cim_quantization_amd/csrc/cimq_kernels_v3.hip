@@ -46,6 +46,17 @@ __device__ inline int fdiv(int n, int d, float inv) {
 
 __device__ inline size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// grad_out of the 4 pixels m4 .. m4+3 (a quad inside one image, m4 % 4 == 0) for channel o,
+// in either layout (Geo::onchw); NCHW makes it one 16-B load
+__device__ inline float4 load_g4(const Geo& g, const float* __restrict__ gout, size_t m4, int o) {
+  if (g.onchw) {
+    const size_t b = m4 / g.P, p = m4 - b * g.P;
+    return *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p);
+  }
+  return make_float4(gout[m4 * g.O + o], gout[(m4 + 1) * g.O + o], gout[(m4 + 2) * g.O + o],
+                     gout[(m4 + 3) * g.O + o]);
+}
+
 // Batched global -> LDS copy: every thread issues U independent loads before its first LDS
 // store, so a block waits about one memory latency per U*blockDim elements instead of one
 // per element.  src(idx) returns element idx; it lands in dst[idx].
@@ -418,7 +429,14 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const int o = (og * 4 + ob) * 16 + r16;
       if (ob < nob && o < g.O) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[((size_t)mt * 64 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[ob][r];
+        for (int r = 0; r < 4; ++r)
+          if (!g.onchw) out[((size_t)mt * 64 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[ob][r];
+        if (g.onchw) {
+          const size_t m4 = (size_t)mt * 64 + wave * 16 + 4 * g4;
+          const size_t bb = m4 / g.P, pq = m4 - bb * g.P;
+          *reinterpret_cast<float4*>(out + (bb * g.O + o) * g.P + pq) =
+              make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+        }
       }
     }
   }
@@ -603,15 +621,24 @@ __global__ __launch_bounds__(512, 2) void cim_bwd_gx_v5_kernel(Geo g, V3 v, cons
               }
           }
           float gv[4][4];
+          if (g.onchw) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float* grow = gout + (m0 + r) * g.O;
-            if (gvec && o0 + 4 <= g.O) {
-              const float4 t4 = *reinterpret_cast<const float4*>(grow + o0);
-              gv[r][0] = t4.x; gv[r][1] = t4.y; gv[r][2] = t4.z; gv[r][3] = t4.w;
-            } else {
+            for (int e = 0; e < 4; ++e) {
+              float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (o0 + e < g.O) t4 = load_g4(g, gout, m0, o0 + e);
+              gv[0][e] = t4.x; gv[1][e] = t4.y; gv[2][e] = t4.z; gv[3][e] = t4.w;
+            }
+          } else {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) gv[r][e] = (o0 + e < g.O) ? grow[o0 + e] : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              const float* grow = gout + (m0 + r) * g.O;
+              if (gvec && o0 + 4 <= g.O) {
+                const float4 t4 = *reinterpret_cast<const float4*>(grow + o0);
+                gv[r][0] = t4.x; gv[r][1] = t4.y; gv[r][2] = t4.z; gv[r][3] = t4.w;
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gv[r][e] = (o0 + e < g.O) ? grow[o0 + e] : 0.f;
+              }
             }
           }
 #pragma unroll
@@ -1102,8 +1129,8 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
   auto load_in = [&](int m0, float (&gd)[4], uint32_t (&sd)[NBWX][SWD]) {
     const bool ok = m0 < mend && ocol;
     const size_t mq = ((size_t)m0 >> 2) + wave * 4 + g4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gd[r] = ok ? gout[(size_t)(m0 + wave * 16 + 4 * g4 + r) * g.O + o] : 0.f;
+    const float4 g4v = ok ? load_g4(g, gout, (size_t)m0 + wave * 16 + 4 * g4, o) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gd[0] = g4v.x; gd[1] = g4v.y; gd[2] = g4v.z; gd[3] = g4v.w;
 #pragma unroll
     for (int k = 0; k < NBWX; ++k) {
 #pragma unroll
@@ -1254,9 +1281,11 @@ __global__ __launch_bounds__(256) void cim_galpha_v5_kernel(Geo g, const uint8_t
       const uint4 w = reinterpret_cast<const uint4*>(st)[e];
       sv[0] = w.x; sv[1] = w.y; sv[2] = w.z; sv[3] = w.w;
     }
+    const float4 g4v = load_g4(g, gout, (size_t)q * 4, o);
+    const float gq[4] = {g4v.x, g4v.y, g4v.z, g4v.w};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float gv = gout[((size_t)q * 4 + r) * g.O + o];
+      const float gv = gq[r];
 #pragma unroll
       for (int j = 0; j < NBP; ++j) {
         const uint32_t bits = sv[r] >> (3 * j);

@@ -163,6 +163,76 @@ def cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, pad
                                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar)
 
 
+class _CimModuleConv(torch.autograd.Function):
+    """A whole Conv2dLSQCiM layer after its first-step init (lsq.py:544-581): the activation,
+    weight and alpha_cim quantisers run inside libcimq on the raw parameters (no torch ops,
+    no materialised x_q / w_q / alpha_q tensors); returns the NCHW output."""
+
+    @staticmethod
+    def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
+                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha):
+        _require_device(x)
+        dev = x.device
+        B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
+        qp_a = float(2 ** nbits_a - 1)
+        qn_w, qp_w = -(2 ** (nbits_w - 1)), 2 ** (nbits_w - 1) - 1
+        desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
+                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a)
+        lsq = _lib.make_lsq_desc(qn_w, qp_w, 1.0 / math.sqrt(x.numel() * qp_a),
+                                 1.0 / math.sqrt(weight.numel() * qp_w),
+                                 nbits_alpha if alpha_cim is not None else 0)
+        sizes = _lib.query_sizes(desc)
+        xc = x.detach().to(torch.float32).contiguous()
+        wc = weight.detach().to(torch.float32).contiguous()
+        aa = alpha_act.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        aw = alpha_weight.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        ac = None if alpha_cim is None else alpha_cim.detach().to(torch.float32).contiguous()
+        bm = binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+        sg = signed_act.detach().to(device=dev, dtype=torch.float32).reshape(-1)[:1].contiguous()
+        Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+        Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+        out = torch.empty(B, O, Ho, Wo, device=dev, dtype=torch.float32)
+        cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+        ws = torch.empty(max(sizes.fwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_module_forward(desc, lsq, xc.data_ptr(), wc.data_ptr(), aa.data_ptr(), aw.data_ptr(),
+                                           None if ac is None else ac.data_ptr(), bm.data_ptr(), sg.data_ptr(),
+                                           out.data_ptr(), cbuf.data_ptr(), ws.data_ptr(), _stream()),
+                   "cimq_module_forward")
+        ctx.desc, ctx.lsq, ctx.sizes = desc, lsq, sizes
+        ctx.bufs = (xc, wc, aa, aw, ac, bm, sg, cbuf)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        xc, wc, aa, aw, ac, bm, sg, cbuf = ctx.bufs
+        dev = xc.device
+        g = grad_output.detach().to(torch.float32).contiguous()
+        gx = torch.empty_like(xc)
+        gw = torch.empty_like(wc)
+        gaa = torch.empty(1, device=dev, dtype=torch.float32)
+        gaw = torch.empty(1, device=dev, dtype=torch.float32)
+        gac = None if ac is None else torch.empty_like(ac)
+        ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        lib = _lib.load()
+        _lib.check(lib.cimq_module_backward(ctx.desc, ctx.lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
+                                            aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),
+                                            bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(),
+                                            gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
+                                            None if gac is None else gac.data_ptr(), ws.data_ptr(), _stream()),
+                   "cimq_module_backward")
+        return (gx, gw, gaa, gaw, gac) + (None,) * 12
+
+
+def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
+                    dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha):
+    """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
+    the three step-size parameters (alpha_act and alpha_weight are 1-element tensors)."""
+    return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
+                                padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
+                                nbits_alpha)
+
+
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,
                    nbits_w, wbitslice, adcbits, xbar, num_xbars):
     """First-step alpha_cim initialisation on the device (lsq.py:557-563, 35-87)."""

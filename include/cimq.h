@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 1
+#define CIMQ_ABI_VERSION 2
 
 /* status codes */
 #define CIMQ_OK 0
@@ -62,6 +62,15 @@ typedef struct cimq_conv_desc {
   float lsq_qp;       /* CIMQ_INPUT_RAW_LSQ: act clamp max Qp_a = 2^bits_a - 1 (Qn_a = 0) */
   int32_t reserved[4];
 } cimq_conv_desc;
+
+/* The LSQ quantisers of Conv2dLSQCiM.forward (lsq.py:544-571), for the module entry points. */
+typedef struct cimq_lsq_desc {
+  float qn_w, qp_w;         /* weight clamp range: -2^(bits_w-1), 2^(bits_w-1)-1 (lsq.py:553-555) */
+  float gscale_a;           /* grad_scale factor of alpha_act: 1/sqrt(numel(x) * Qp_a) (lsq.py:547) */
+  float gscale_w;           /* grad_scale factor of alpha_weight: 1/sqrt(numel(w) * Qp_w) (lsq.py:553) */
+  int32_t nbits_alpha;      /* alpha_cim quantiser bits (lsq.py:566-571); ignored unless adc 1 / 1.5 */
+  int32_t reserved[3];
+} cimq_lsq_desc;
 
 typedef struct cimq_sizes {
   size_t ctx_bytes;           /* forward -> backward state, caller-owned device memory */
@@ -101,6 +110,26 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
                   const float* sw, const float* alpha_q, const int8_t* binary_mask,
                   const float* signed_act, const void* ctx, float* grad_x, float* grad_w,
                   float* grad_alpha, float* grad_sa, void* ws, void* stream);
+
+/* Forward of a whole Conv2dLSQCiM layer after its first-step initialisation (lsq.py:544-581):
+ * the activation, weight and alpha_cim quantisers run inside the library on the raw
+ * parameters, then the CiM conv; ``out`` is the module's NCHW output [B, O, Ho, Wo] (before
+ * the optional bias).  Requires input_kind = CIMQ_INPUT_RAW_LSQ.  ``alpha_cim`` may be NULL
+ * unless adc_bits is 1 or 1.5.  ``ctx`` must hold cimq_query_sizes()->ctx_bytes and ``ws``
+ * fwd_workspace_bytes. */
+int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                        const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                        const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
+                        void* stream);
+
+/* Backward of cimq_module_forward: from d loss / d out (NCHW) to the gradients of the raw
+ * activation and of the four parameters (weight, alpha_act, alpha_weight, alpha_cim), through
+ * the quantisers as torch's autograd differentiates them. */
+int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out, const float* x,
+                         const float* weight, const float* alpha_act, const float* alpha_weight,
+                         const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,
+                         const void* ctx, float* grad_x, float* grad_weight, float* grad_alpha_act,
+                         float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
 
 /* First-step alpha_cim initialisation (lsq.py:557-563 with get_analog_partial_sums_signed,
  * lsq.py:35-87): alpha_init[1,T,nbw,nba,1,O] = 2*mean_{b,p}|ps*sw*sa| / sqrt(Qp_adc), zeros
