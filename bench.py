@@ -72,20 +72,15 @@ class Trainer:
     alpha_* excluded from weight decay)."""
 
     def __init__(self, layers, world):
+        from cim_quantization_amd.dist import GradBucket
         self.layers, self.world = layers, world
-        params = [p for m in layers for p in m.parameters()]
-        n = sum(p.numel() for p in params)
-        dev = params[0].device
-        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
-        off = 0
-        for p in params:  # gradients live in one bucket: one all-reduce per step
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
+        self.bucket = GradBucket([p for m in layers for p in m.parameters()])  # one all-reduce per step
+        self.flat = self.bucket.flat
         decay = [p for m in layers for nm, p in m.named_parameters() if not nm.startswith("alpha")]
         no_decay = [p for m in layers for nm, p in m.named_parameters() if nm.startswith("alpha")]
         self.opt = torch.optim.SGD([{"params": decay, "weight_decay": 1e-4},
                                     {"params": no_decay, "weight_decay": 0.0}], lr=0.01, momentum=0.9)
-        self.bucket_mb = n * 4 / 1e6
+        self.bucket_mb = self.bucket.nbytes / 1e6
 
     def compute(self, xs, gs):
         """fwd + bwd of every layer; gradients accumulate into the flat bucket."""
@@ -94,9 +89,7 @@ class Trainer:
 
     def finish(self):
         """gradient exchange (one RCCL all-reduce of the bucket) + SGD update."""
-        if self.world > 1:
-            dist.all_reduce(self.flat)
-            self.flat.mul_(1.0 / self.world)
+        self.bucket.exchange()
         self.opt.step()
         self.flat.zero_()
 
