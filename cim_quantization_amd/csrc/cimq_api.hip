@@ -253,7 +253,8 @@ Plan3 v3_plan(const Geo& g) {
   const size_t pg = a16((size_t)v.NCG * v.RH * v.WP * g.NBP);
   const size_t gw_tail = (size_t)g.KS * 64 * 4 + (size_t)g.nbw * nog * g.KS * 1024 + (size_t)nkj * nog * 16 * 16 +
                          a16((size_t)nkj * 32 * 4) + ckl;
-  p.lds_gw = std::max(a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + 128 * 4 + ckl;
+  p.lds_gw = std::max(a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + 128 * 4 +
+             a16((size_t)nkj * 16 * 4) + ckl;
   p.lds_init = pg + gw_tail;
   const size_t lim = kLdsMax - 512;
   p.ok = p.lds_fwd <= lim && p.lds_gx <= lim && p.lds_gw <= lim;
@@ -424,14 +425,9 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     CIMQ_TRY(set_lds(kern, p.lds_gw));
     dim3 grid16(W.nchunks, g.T, g.OB16);
     hipLaunchKernelGGL(kern, grid16, dim3(256), p.lds_gw, s, g, p.v, ctx + L.st, ctx + L.xhat, pp, gout, W.rows,
-                       reinterpret_cast<float*>(ws + W.gw_slab));
+                       reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
     prof_end(slot, s);
-    CIMQ_TRY(check_hip("cim_bwd_gw_v5"));
-    if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
-      hipLaunchKernelGGL(cim_galpha_v5_kernel<NBP>, dim3(W.nchunks, g.T * g.nbw), dim3(256), 0, s, g, ctx + L.st,
-                         gout, W.rows, reinterpret_cast<float*>(ws + W.ga_slab));
-    }
-    return check_hip("cim_galpha_v5");
+    return check_hip("cim_bwd_gw_v5");
   } else if (p.ok) {
     const size_t lds = p.lds_init;
     auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, INIT> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, INIT>;
@@ -529,7 +525,7 @@ int launch_reduce_galpha(const Geo& g, const uint8_t* ctx, uint8_t* ws, float cg
                          const float* sa, float* out, hipStream_t s) {
   WsLayout W = ws_layout(g);
   const long long nout = (long long)g.T * g.nbw * g.nba * g.Opad;
-  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(256), 0, s, g, W.nchunks,
+  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks,
                      reinterpret_cast<const float*>(ws + W.ga_slab), params_of(g, const_cast<uint8_t*>(ctx)),
                      cgrad, init, sw, sa, (float)((double)g.B * g.P), (float)sqrt((double)g.qp), out);
   return check_hip("reduce_galpha");
@@ -608,7 +604,7 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   WsLayout W = ws_layout(g);
   {
     const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
-    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(256), 0, s, g, W.nchunks,
+    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks,
                        reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
     CIMQ_TRY(check_hip("reduce_gw"));
   }
@@ -734,7 +730,7 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
   const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
   const int nwb = cdiv(nout, 64);
   float* wpart = reinterpret_cast<float*>(w + W.wpart);
-  hipLaunchKernelGGL(reduce_gw_lsq_kernel, dim3(nwb), dim3(256), 0, s, g, la, W.nchunks,
+  hipLaunchKernelGGL(reduce_gw_lsq_kernel, dim3(nwb), dim3(1024), 0, s, g, la, W.nchunks,
                      reinterpret_cast<const float*>(w + W.gw_slab), scal, weight, grad_weight, wpart);
   CIMQ_TRY(check_hip("reduce_gw_lsq"));
   if (has_alpha) {

@@ -1082,7 +1082,7 @@ template <int NBP, int FBX, int NBWX>
 __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
                                                                const uint8_t* __restrict__ xcb, Params pp,
                                                                const float* __restrict__ gout, int rows_per_chunk,
-                                                               float* __restrict__ gw_slab) {
+                                                               float* __restrict__ gw_slab, float* __restrict__ ga_slab) {
   constexpr int NS = NBP / 2;
   constexpr int SWD = NBP / 2;  // state dwords per (pixel quad, channel): 4 x uint16 or 4 x uint32
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1099,6 +1099,7 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
   float* gwacc = reinterpret_cast<float*>(cur);  // aliases the patch after the pixel loop
   cur += max(pbsz, gwsz);
   int* ptab = reinterpret_cast<int*>(cur); cur += 128 * 4;
+  float* qacc = reinterpret_cast<float*>(cur); cur += al16((size_t)nkj * 16 * 4);  // [kj][16 channels]
   float* ckl = reinterpret_cast<float*>(cur);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1110,6 +1111,8 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
   const bool ocol = o < g.O;
 
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
+  for (int t = threadIdx.x; t < nkj * 16; t += blockDim.x) qacc[t] = 0.f;
+  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
   build_ptab(g, i, 2, v.RH, v.WP, ptab, c0);
   zero_lds(reinterpret_cast<uint32_t*>(patchB), (int)(pbsz / 4));
   __syncthreads();
@@ -1159,6 +1162,12 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
   v4f gwa[FBX];
 #pragma unroll
   for (int a = 0; a < FBX; ++a) gwa[a] = v4f{0.f, 0.f, 0.f, 0.f};
+  // grad_alpha_cim partial sums (lsq.py:321-333): sum over this lane's pixels of code * g
+  float qs[NBWX][NBP];
+#pragma unroll
+  for (int kk = 0; kk < NBWX; ++kk)
+#pragma unroll
+    for (int j = 0; j < NBP; ++j) qs[kk][j] = 0.f;
   const int tiles_per_img = g.P >> 6;
 
   for (int m0 = mbeg; m0 < mend; m0 += 64) {
@@ -1191,7 +1200,11 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
           if (j < g.nba) {
             const float cd = ckl[2 * nkj + k * g.nba + j];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) D[j][r] += ((word(scur, k, r) >> (3 * j)) & 1u) ? cd : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t bits = word(scur, k, r) >> (3 * j);
+              D[j][r] += (bits & 1u) ? cd : 0.f;
+              qs[k][j] += (bits & 2u) ? ((bits & 4u) ? -gcur[r] : gcur[r]) : 0.f;
+            }
           }
         }
       }
@@ -1244,6 +1257,25 @@ __global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
       for (int r = 0; r < 4; ++r) atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * 16 + r16], gwa[fb][r]);
   __syncthreads();
   const int mc = blockIdx.x;
+  if (has_code) {
+#pragma unroll
+    for (int kk = 0; kk < NBWX; ++kk) {
+#pragma unroll
+      for (int j = 0; j < NBP; ++j) {
+        if (kk < g.nbw && j < g.nba) {
+          float q = qs[kk][j];
+          q += __shfl_xor(q, 16);
+          q += __shfl_xor(q, 32);
+          if (g4 == 0) atomicAdd(&qacc[(kk * g.nba + j) * 16 + r16], q);
+        }
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nkj * 16; t += blockDim.x) {
+      const int kj = t >> 4, col = t & 15;
+      ga_slab[(((size_t)mc * g.T + i) * nkj + kj) * g.Opad + ob * 16 + col] = qacc[t];
+    }
+  }
   for (int t = threadIdx.x; t < g.FBT * 16 * 16; t += blockDim.x) {
     const int fl = t >> 4, col = t & 15;
     const int oo = ob * 16 + col;
@@ -1308,22 +1340,32 @@ __global__ __launch_bounds__(256) void cim_galpha_v5_kernel(Geo g, const uint8_t
 // ---------------------------------------------------------------------------------------
 // coalesced, thread-parallel slab reductions: 64 consecutive outputs x 4 chunk lanes / block
 // ---------------------------------------------------------------------------------------
+// 64 consecutive outputs per block, blockDim/64 chunk lanes per output; every lane keeps four
+// independent loads in flight.  Returns the sum in the threads of the first wave.
 __device__ inline float reduce_chunks(const float* __restrict__ slab, size_t chunk_stride, int nchunks,
                                       size_t idx, float* red) {
-  const int sub = threadIdx.x >> 6;  // 0..3
-  float s = 0.f;
-  for (int c = sub; c < nchunks; c += 4) s += slab[(size_t)c * chunk_stride + idx];
-  red[threadIdx.x] = s;
+  const int sub = threadIdx.x >> 6, nsub = blockDim.x >> 6;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int c = sub;
+  for (; c + 3 * nsub < nchunks; c += 4 * nsub) {
+    a0 += slab[(size_t)c * chunk_stride + idx];
+    a1 += slab[(size_t)(c + nsub) * chunk_stride + idx];
+    a2 += slab[(size_t)(c + 2 * nsub) * chunk_stride + idx];
+    a3 += slab[(size_t)(c + 3 * nsub) * chunk_stride + idx];
+  }
+  for (; c < nchunks; c += nsub) a0 += slab[(size_t)c * chunk_stride + idx];
+  red[threadIdx.x] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   float v = 0.f;
-  if (sub == 0) v = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+  if (sub == 0)
+    for (int t = 0; t < nsub; ++t) v += red[threadIdx.x + 64 * t];
   return v;
 }
 
-__global__ __launch_bounds__(256) void reduce_gw_v3_kernel(Geo g, int nchunks, const float* __restrict__ gw_slab,
-                                                           const float* __restrict__ sa_p,
-                                                           float* __restrict__ grad_w) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(1024) void reduce_gw_v3_kernel(Geo g, int nchunks, const float* __restrict__ gw_slab,
+                                                            const float* __restrict__ sa_p,
+                                                            float* __restrict__ grad_w) {
+  __shared__ float red[1024];
   const size_t rows = (size_t)g.T * g.FBT * 16;  // (tile, f-in-tile)
   const size_t nout = rows * g.Opad;
   const size_t idx = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
@@ -1337,12 +1379,12 @@ __global__ __launch_bounds__(256) void reduce_gw_v3_kernel(Geo g, int nchunks, c
   }
 }
 
-__global__ __launch_bounds__(256) void reduce_galpha_v3_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab,
-                                                               Params pp, float cgrad, int init,
-                                                               const float* __restrict__ sw_p,
-                                                               const float* __restrict__ sa_p, float count,
-                                                               float sqrt_qp, float* __restrict__ out) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(1024) void reduce_galpha_v3_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab,
+                                                                Params pp, float cgrad, int init,
+                                                                const float* __restrict__ sw_p,
+                                                                const float* __restrict__ sa_p, float count,
+                                                                float sqrt_qp, float* __restrict__ out) {
+  __shared__ float red[1024];
   const int nkj = g.nbw * g.nba;
   const size_t nout = (size_t)g.T * nkj * g.Opad;
   const size_t idx = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);

@@ -121,25 +121,21 @@ __global__ __launch_bounds__(1024) void prep_lsq_kernel(Geo g, LsqArgs q, const 
 // then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
 //   grad_weight = mask * (G * sw) / sw; partial sums of G * rp (MulBackward, d/d sw) and of
 //   -grad_t1 * ((w / sw) / sw) (DivBackward wrt the divisor) per block -> wpart[2*block].
-__global__ __launch_bounds__(256) void reduce_gw_lsq_kernel(Geo g, LsqArgs q, int nchunks,
-                                                            const float* __restrict__ gw_slab,
-                                                            const float* __restrict__ scal,
-                                                            const float* __restrict__ weight,
-                                                            float* __restrict__ grad_weight,
-                                                            float* __restrict__ wpart) {
-  __shared__ float red[256];
+__global__ __launch_bounds__(1024) void reduce_gw_lsq_kernel(Geo g, LsqArgs q, int nchunks,
+                                                             const float* __restrict__ gw_slab,
+                                                             const float* __restrict__ scal,
+                                                             const float* __restrict__ weight,
+                                                             float* __restrict__ grad_weight,
+                                                             float* __restrict__ wpart) {
+  __shared__ float red[1024];
   const size_t rows = (size_t)g.T * g.FBT * 16;
   const size_t nout = rows * g.Opad;
   const size_t idx = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const int sub = threadIdx.x >> 6;
-  float s = 0.f;
-  if (idx < nout)
-    for (int c = sub; c < nchunks; c += 4) s += gw_slab[(size_t)c * nout + idx];
-  red[threadIdx.x] = s;
-  __syncthreads();
+  const float vsum = reduce_chunks(gw_slab, nout, nchunks, idx < nout ? idx : 0, red);
   float p_mul = 0.f, p_div = 0.f;
   if (sub == 0 && idx < nout) {
-    const float v = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    const float v = vsum;
     const int o = (int)(idx % g.Opad);
     const size_t row = idx / g.Opad;
     const int i = (int)(row / (g.FBT * 16)), fl = (int)(row - (size_t)i * g.FBT * 16);
