@@ -75,6 +75,7 @@ class Trainer:
         from cim_quantization_amd.dist import GradBucket
         self.layers, self.world = layers, world
         self.bucket = GradBucket([p for m in layers for p in m.parameters()])  # one all-reduce per step
+        self.bucket.own(layers)  # the layers add their grads straight into the bucket
         self.flat = self.bucket.flat
         decay = [p for m in layers for nm, p in m.named_parameters() if not nm.startswith("alpha")]
         no_decay = [p for m in layers for nm, p in m.named_parameters() if nm.startswith("alpha")]

@@ -13,10 +13,11 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
+CIMQ_LSQ_ACCUMULATE_GRADS = 1
 
 # every symbol include/cimq.h declares
 EXPORTED_SYMBOLS = (
@@ -60,7 +61,8 @@ class LsqDesc(ctypes.Structure):
     """Mirror of ``cimq_lsq_desc``."""
 
     _fields_ = [("qn_w", ctypes.c_float), ("qp_w", ctypes.c_float), ("gscale_a", ctypes.c_float),
-                ("gscale_w", ctypes.c_float), ("nbits_alpha", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("gscale_w", ctypes.c_float), ("nbits_alpha", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 class Sizes(ctypes.Structure):
@@ -148,11 +150,12 @@ def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w
     return d
 
 
-def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha) -> LsqDesc:
+def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha, flags=0) -> LsqDesc:
     q = LsqDesc()
     q.qn_w, q.qp_w = float(qn_w), float(qp_w)
     q.gscale_a, q.gscale_w = float(gscale_a), float(gscale_w)
     q.nbits_alpha = int(nbits_alpha)
+    q.flags = int(flags)
     return q
 
 

@@ -50,6 +50,9 @@ class Conv2dLSQCiM(_Conv2dQCiM):
                          abitslice=abitslice, xbar=xbar, adcbits=adcbits, stochastic_quant=stochastic_quant)
         self._state_cache = None  # host mirror of (init_state, init_state_cim) to avoid a sync per step
         self.fused = True  # steady state through cimq_module_forward/backward (False: torch quantisers)
+        # parameter grads added into the existing .grad buffers inside the library (no
+        # AccumulateGrad kernels); set by dist.GradBucket.own(), which owns the exchange
+        self.accumulate_grads_in_place = False
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
@@ -81,7 +84,7 @@ class Conv2dLSQCiM(_Conv2dQCiM):
             out = cim_module_conv(x, self.weight, self.alpha_act, self.alpha_weight, self.alpha_cim,
                                   self.binary_mask, self.signed_act, self.stride, self.padding, self.dilation,
                                   self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
-                                  self.xbar, self.nbits_alpha)
+                                  self.xbar, self.nbits_alpha, self.accumulate_grads_in_place)
             if self.bias is not None:
                 out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
             return out

@@ -108,7 +108,7 @@ int make_geo(const cimq_conv_desc* d, Geo* out) {
 
 struct CtxLayout {
   size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st;
-  size_t lsq_scal, lsq_wq, lsq_aq;  // module entry points: sa/sw/alpha scale, w_q, alpha_q
+  size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t total;
 };
 
@@ -132,8 +132,6 @@ CtxLayout ctx_layout(const Geo& g) {
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   L.st = o; o = align256(o + (size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4));
   L.lsq_scal = o; o = align256(o + 16 * 4);
-  L.lsq_wq = o; o = align256(o + (size_t)g.O * g.K * 4);
-  L.lsq_aq = o; o = align256(o + npar * 4);
   L.total = o;
   return L;
 }
@@ -643,6 +641,7 @@ static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   a->gs_w = q->gscale_w;
   a->nbits_alpha = q->nbits_alpha;
   a->nalpha = g.T * g.nbw * g.nba * g.O;
+  if (q->flags & ~CIMQ_LSQ_ACCUMULATE_GRADS) return fail(CIMQ_EINVAL, "unknown LSQ flags 0x%x", q->flags);
   return CIMQ_OK;
 }
 
@@ -664,12 +663,35 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
   CtxLayout L = ctx_layout(g);
   float* scal = reinterpret_cast<float*>(c + L.lsq_scal);
-  float* wq = reinterpret_cast<float*>(c + L.lsq_wq);
-  float* aq = reinterpret_cast<float*>(c + L.lsq_aq);
-  hipLaunchKernelGGL(prep_lsq_kernel, dim3(1), dim3(1024), 0, s, g, la, alpha_act, alpha_weight, weight,
-                     alpha_cim, scal, wq, aq);
-  CIMQ_TRY(check_hip("prep_lsq"));
-  CIMQ_TRY(prep_all(g, x, wq, scal, scal + 1, has_alpha ? aq : nullptr, binary_mask, signed_act, c, s, true, true));
+  {
+    const bool fast = v3_plan(g).ok;
+    ModulePrep a;
+    a.x = x;
+    a.alpha_act = alpha_act;
+    a.alpha_w = alpha_weight;
+    a.weight = weight;
+    a.alpha_cim = has_alpha ? alpha_cim : nullptr;
+    a.signed_act = signed_act;
+    a.bmask = binary_mask;
+    a.xcf = c + L.xcode;
+    a.xcb = c + L.xhat;
+    a.wfrag = reinterpret_cast<v4i*>(c + L.wfrag);
+    a.wgx = reinterpret_cast<v4i*>(c + L.wgx);
+    a.wtc = reinterpret_cast<uint4*>(c + L.wtc);
+    a.Cp = (g.C + 15) / 16 * 16;
+    a.pp = params_of(g, c);
+    a.scal = scal;
+    a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 256), 8192);
+    a.nwf = g.T * g.KS * g.NBLK * 64;
+    a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;  // general grad_x kernel operand
+    a.nwt = fast ? g.KHW * a.Cp * g.NKS * 4 : 0;  // fast grad_x kernel operand
+    a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+    const int nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.npp, 256), 1024));
+    const int slot = prof_begin(KID_PREP_ACT, g, s);
+    hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, a);
+    prof_end(slot, s);
+    CIMQ_TRY(check_hip("prep_module"));
+  }
   const Plan3 p = v3_plan(g);
   if (p.ok) {
     g.onchw = 1;
@@ -726,21 +748,7 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
   bool lsq_fused = false;
   if (g.NBP == 4) CIMQ_TRY(dispatch_bwd<4>(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused));
   else CIMQ_TRY(dispatch_bwd<8>(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused));
-  // grad_w fused with the weight quantiser's backward
-  const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
-  const int nwb = cdiv(nout, 64);
-  float* wpart = reinterpret_cast<float*>(w + W.wpart);
-  hipLaunchKernelGGL(reduce_gw_lsq_kernel, dim3(nwb), dim3(1024), 0, s, g, la, W.nchunks,
-                     reinterpret_cast<const float*>(w + W.gw_slab), scal, weight, grad_weight, wpart);
-  CIMQ_TRY(check_hip("reduce_gw_lsq"));
-  if (has_alpha) {
-    const double numel = (double)g.B * g.T * g.nbw * g.nba * g.P * g.O;
-    const float cgrad = (float)(1.0 / sqrt(numel * (double)g.qp));  // lsq.py:323,330
-    float* gaq = reinterpret_cast<float*>(w + W.gaq);
-    CIMQ_TRY(launch_reduce_galpha(g, c, w, cgrad, 0, sw, sa, gaq, s));
-    hipLaunchKernelGGL(alpha_cim_bwd_kernel, dim3(1), dim3(1024), 0, s, la, alpha_cim, scal, gaq, grad_alpha_cim);
-    CIMQ_TRY(check_hip("alpha_cim_bwd"));
-  }
+  // the act-LSQ partials: fused into the fast grad_x kernel, a separate pass otherwise
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
   if (lsq_fused) {
@@ -752,9 +760,31 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
     CIMQ_TRY(check_hip("lsq_act_bwd"));
     nparts = grid;
   }
-  hipLaunchKernelGGL(lsq_scalars_finish_kernel, dim3(1), dim3(1024), 0, s, la, nwb, wpart, nparts, part,
-                     grad_alpha_weight, grad_alpha_act);
-  return check_hip("lsq_scalars_finish");
+  // one epilogue launch: grad_w + weight-LSQ backward, grad_alpha_cim, the step-size grads
+  ModuleTail a;
+  a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
+  a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
+  a.scal = scal;
+  a.weight = weight;
+  a.alpha_cim = alpha_cim;
+  a.apart = part;
+  a.wpart = reinterpret_cast<float*>(w + W.wpart);
+  a.gaq = reinterpret_cast<float*>(w + W.gaq);
+  a.grad_weight = grad_weight;
+  a.grad_alpha_act = grad_alpha_act;
+  a.grad_alpha_w = grad_alpha_weight;
+  a.grad_alpha_cim = grad_alpha_cim;
+  a.pp = params_of(g, const_cast<uint8_t*>(c));
+  a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
+  a.nchunks = W.nchunks;
+  a.nwb = cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64);
+  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
+  a.napart = nparts;
+  a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
+  hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(a.nwb + a.nga), dim3(1024), 0, s, g, la, a);
+  CIMQ_TRY(check_hip("module_bwd_tail"));
+  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, la, a);
+  return check_hip("module_bwd_finish");
 }
 
 int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,

@@ -97,6 +97,19 @@ __device__ inline float clamp_nan(float v, float lo, float hi) {
 }
 
 // The fp16 store of the partial sums (lsq.py:169,177): an integer ps rounded to half.
+// grad_scale(x, s) forward value: (x - x*s).detach() + x*s  (_quan_base.py grad_scale)
+__device__ inline float grad_scale_value(float x, float s) {
+  const float yg = x * s;
+  const float d = x - yg;
+  return d + yg;
+}
+
+// round_pass(v) forward value: (v.round() - v).detach() + v  (lsq.py:29-32)
+__device__ inline float round_pass_value(float v) {
+  const float r = rintf(v);
+  return (r - v) + v;
+}
+
 __device__ inline float ps_half(int p) { return __half2float(__float2half_rn((float)p)); }
 
 // u = ps * sw * sa in fp32, in the reference's order (lsq.py:195).

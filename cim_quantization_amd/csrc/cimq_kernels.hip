@@ -42,41 +42,44 @@ __device__ inline void pack_word(int8_t (&v)[8], int nbp, uint8_t* dst, long lon
   }
 }
 
+__device__ inline void act_item(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
+                                uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long idx) {
+  float v = x[idx];
+  float xq;
+  if (g.input_kind == 1) {
+    float t = v / sa;
+    float c = clamp_nan(t, 0.f, g.lsq_qp);
+    float r = rintf(c);
+    float rp = (r - c) + c;  // round_pass value
+    xq = rp * sa;
+  } else {
+    xq = v;
+  }
+  const float xi = xq / sa;
+  const float xh = (float)to_i8_wrap(xi);
+  int8_t fw[8], bw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = 0.f, sb = 0.f;
+    if (j < g.nba) {
+      s = sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa);
+      sb = sgn ? slice_signed(xh, j, g.bsa) : slice_unsigned(xh, j, g.bsa);
+    }
+    fw[j] = (j < g.nba) ? (int8_t)clamp_i8(s) : (int8_t)0;
+    bw[j] = (j < g.nba) ? (int8_t)clamp_i8(sb) : (int8_t)0;
+  }
+  pack_word(fw, g.NBP, xcf, idx);
+  pack_word(bw, g.NBP, xcb, idx);
+}
+
 __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ sa_p,
                                 const float* __restrict__ signed_p, uint8_t* __restrict__ xcf,
                                 uint8_t* __restrict__ xcb) {
   const float sa = *sa_p;
   const bool sgn = (*signed_p) != 0.f;
-  const long long n = g.Nin;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
-       idx += (long long)gridDim.x * blockDim.x) {
-    float v = x[idx];
-    float xq;
-    if (g.input_kind == 1) {
-      float t = v / sa;
-      float c = clamp_nan(t, 0.f, g.lsq_qp);
-      float r = rintf(c);
-      float rp = (r - c) + c;  // round_pass value
-      xq = rp * sa;
-    } else {
-      xq = v;
-    }
-    const float xi = xq / sa;
-    const float xh = (float)to_i8_wrap(xi);
-    int8_t fw[8], bw[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = 0.f, sb = 0.f;
-      if (j < g.nba) {
-        s = sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa);
-        sb = sgn ? slice_signed(xh, j, g.bsa) : slice_unsigned(xh, j, g.bsa);
-      }
-      fw[j] = (j < g.nba) ? (int8_t)clamp_i8(s) : (int8_t)0;
-      bw[j] = (j < g.nba) ? (int8_t)clamp_i8(sb) : (int8_t)0;
-    }
-    pack_word(fw, g.NBP, xcf, idx);
-    pack_word(bw, g.NBP, xcb, idx);
-  }
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < g.Nin;
+       idx += (long long)gridDim.x * blockDim.x)
+    act_item(g, x, sa, sgn, xcf, xcb, idx);
 }
 
 // =========================================================================================
@@ -88,90 +91,115 @@ __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float*
 // rows n = nb*16 + (l&15) (n = k*Opad + o) and contraction f = i*xbar + ks*64 + 16*(l>>4) + e.
 // grad_x operand: int8(slice) (lsq.py:160 truncation) as bf16, wgx[i][fb][s][lane][8]:
 // lane l holds f = i*xbar + fb*16 + (l&15), kappa = (2s + (e>>2))*16 + 4*(l>>4) + (e&3).
-__device__ inline float wslice(const Geo& g, const float* w_q, float sw, int f, int n) {
+// Source of the integer weights w_int = w_q / sw: either a materialised w_q (Function entry
+// points) or the raw weight run through the LSQ quantiser in place (module entry points:
+// w_q = round_pass(clamp(w / sw, Qn, Qp)) * sw, lsq.py:555, the same fp32 op sequence).
+struct WSrc {
+  const float* w;
+  float sw;
+  int raw;
+  float qn, qp;
+  __device__ float wint(const Geo& g, int o, int f) const {
+    const float v = w[(size_t)o * g.K + f];
+    if (!raw) return v / sw;
+    const float c = clamp_nan(v / sw, qn, qp);
+    const float wq = round_pass_value(c) * sw;
+    return wq / sw;
+  }
+};
+
+__device__ inline float wslice(const Geo& g, const WSrc& ws, int f, int n) {
   const int k = n / g.Opad, o = n - k * g.Opad;
   if (f >= g.K || o >= g.O || k >= g.nbw) return 0.f;
-  float wi = w_q[(size_t)o * g.K + f] / sw;
-  return slice_signed(wi, k, g.bsw);
+  return slice_signed(ws.wint(g, o, f), k, g.bsw);
 }
 
-__global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
-                                  v4i* __restrict__ wfrag) {
-  const float sw = *sw_p;
-  const int total = g.T * g.KS * g.NBLK * WAVE;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int lane = t % WAVE;
-    int r = t / WAVE;
-    const int nb = r % g.NBLK;
-    r /= g.NBLK;
-    const int ks = r % g.KS;
-    const int i = r / g.KS;
-    const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
-    const int n = nb * 16 + (lane & 15);
-    uint32_t wd[4] = {0, 0, 0, 0};
+__device__ inline void wfrag_item(const Geo& g, const WSrc& ws, v4i* __restrict__ wfrag, int t) {
+  const int lane = t % WAVE;
+  int r = t / WAVE;
+  const int nb = r % g.NBLK;
+  r /= g.NBLK;
+  const int ks = r % g.KS;
+  const int i = r / g.KS;
+  const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+  const int n = nb * 16 + (lane & 15);
+  uint32_t wd[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int f = flo + ks * 64 + 16 * (lane >> 4) + e;
-      int v = 0;
-      if (f < fhi) v = clamp_i8(wslice(g, w_q, sw, f, n));
-      wd[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
-    }
-    v4i o;
-    o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
-    wfrag[t] = o;
+  for (int e = 0; e < 16; ++e) {
+    const int f = flo + ks * 64 + 16 * (lane >> 4) + e;
+    int v = 0;
+    if (f < fhi) v = clamp_i8(wslice(g, ws, f, n));
+    wd[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
   }
+  v4i o;
+  o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
+  wfrag[t] = o;
 }
 
-__global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
-                                v4i* __restrict__ wgx) {
-  const float sw = *sw_p;
-  const int total = g.T * g.FBT * g.NKS * WAVE;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int lane = t % WAVE;
-    int r = t / WAVE;
-    const int s = r % g.NKS;
-    r /= g.NKS;
-    const int fb = r % g.FBT;
-    const int i = r / g.FBT;
-    const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
-    const int f = flo + fb * 16 + (lane & 15);
-    uint32_t wd[4] = {0, 0, 0, 0};
+__device__ inline void wgx_item(const Geo& g, const WSrc& ws, v4i* __restrict__ wgx, int t) {
+  const int lane = t % WAVE;
+  int r = t / WAVE;
+  const int s = r % g.NKS;
+  r /= g.NKS;
+  const int fb = r % g.FBT;
+  const int i = r / g.FBT;
+  const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+  const int f = flo + fb * 16 + (lane & 15);
+  uint32_t wd[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int kb = 2 * s + (e >> 2);
-      const int kap = kb * 16 + 4 * (lane >> 4) + (e & 3);
-      float v = 0.f;
-      if (f < fhi && kb < g.NBLK) v = (float)to_i8_wrap(wslice(g, w_q, sw, f, kap));
-      const uint32_t h = bf16_bits(v);
-      wd[e >> 1] |= h << (16 * (e & 1));
-    }
-    v4i o;
-    o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
-    wgx[t] = o;
+  for (int e = 0; e < 8; ++e) {
+    const int kb = 2 * s + (e >> 2);
+    const int kap = kb * 16 + 4 * (lane >> 4) + (e & 3);
+    float v = 0.f;
+    if (f < fhi && kb < g.NBLK) v = (float)to_i8_wrap(wslice(g, ws, f, kap));
+    const uint32_t h = bf16_bits(v);
+    wd[e >> 1] |= h << (16 * (e & 1));
   }
+  v4i o;
+  o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
+  wgx[t] = o;
 }
 
 // grad_x transposed-GEMM operand: int8(slice) as bf16 in [khw][c (Cp)][kappa (NKS*32)] order,
 // wtc row (khw, c) = weight row f = c*KHW + khw, so one 16-B piece holds 8 consecutive kappa.
+__device__ inline void wtc_item(const Geo& g, const WSrc& ws, int Cp, uint4* __restrict__ wtc, int t) {
+  const int KAP = g.NKS * 32;
+  const int piece = t % (KAP / 8), row = t / (KAP / 8);
+  const int khw = row / Cp, c = row - khw * Cp;
+  const int f = c * g.KHW + khw;
+  uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int kap = piece * 8 + e;
+    float val = 0.f;
+    if (c < g.C && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, ws, f, kap));
+    wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
+  }
+  wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+}
+
+__global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
+                                  v4i* __restrict__ wfrag) {
+  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
+  const int total = g.T * g.KS * g.NBLK * WAVE;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
+    wfrag_item(g, ws, wfrag, t);
+}
+
+__global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
+                                v4i* __restrict__ wgx) {
+  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
+  const int total = g.T * g.FBT * g.NKS * WAVE;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
+    wgx_item(g, ws, wgx, t);
+}
+
 __global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,
                                 uint4* __restrict__ wtc) {
-  const float sw = *sw_p;
-  const int KAP = g.NKS * 32;
-  const int total = g.KHW * Cp * (KAP / 8);
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int piece = t % (KAP / 8), row = t / (KAP / 8);
-    const int khw = row / Cp, c = row - khw * Cp;
-    const int f = c * g.KHW + khw;
-    uint32_t wd[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int kap = piece * 8 + e;
-      float val = 0.f;
-      if (c < g.C && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, w_q, sw, f, kap));
-      wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
-    }
-    wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-  }
+  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
+  const int total = g.KHW * Cp * (g.NKS * 32 / 8);
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
+    wtc_item(g, ws, Cp, wtc, t);
 }
 
 // =========================================================================================
@@ -204,69 +232,93 @@ __device__ inline int last_true_ternary_lo(int lo, int hi, float sw, float sa, f
   return L;
 }
 
+// Source of alpha_q: a materialised alpha_q, or alpha_cim through its quantiser in place
+// (alpha_q = clamp(round_pass(a / scale), 1, 2^b - 1) * scale, lsq.py:566-571).
+struct ASrc {
+  const float* a;
+  int raw;
+  float scale, qp_al;
+  __device__ float get(int e) const {
+    if (!raw) return a[e];
+    const float t = a[e] / scale;
+    return clamp_nan(round_pass_value(t), 1.f, qp_al) * scale;
+  }
+};
+
+__device__ inline bool scales_ok(float sw, float sa) {
+  return (sw * sa > 0.f) && isfinite(sw * sa) && isfinite(sw) && isfinite(sa);
+}
+
+// one (i, j, k, o) entry (t < npar) or one (k, j) coefficient triple (t >= npar); returns
+// whether the entry needs the literal ADC
+__device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float sa,
+                                   const int8_t* __restrict__ bmask, const Params& pp, int t) {
+  const int npar = g.T * g.nba * g.nbw * g.Opad;
+  const int nkj = g.nbw * g.nba;
+  if (t >= npar) {  // per-(k,j) float coefficients
+    const int kj = t - npar, k = kj / g.nba, j = kj - k * g.nba;
+    const float mk = (float)bmask[k * g.nba + j];  // binary_mask[0,0,k,j,0,0]
+    pp.ckj[kj] = mk;
+    pp.ckj[nkj + kj] = mk * pow2f(-g.bsa * j);      // E weight: 2^-(bsa*j) * mask
+    pp.ckj[2 * nkj + kj] = mk * pow2f(-g.bsw * k);  // D weight: 2^-(bsw*k) * mask
+    return false;
+  }
+  int r = t;
+  const int o = r % g.Opad; r /= g.Opad;
+  const int k = r % g.nbw; r /= g.nbw;
+  const int j = r % g.nba;
+  const int i = r / g.nba;
+  const float mk = (float)bmask[k * g.nba + j];
+  float a = 1.f;
+  if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && as.a != nullptr && o < g.O)
+    a = as.get(((i * g.nbw + k) * g.nba + j) * g.O + o);  // alpha[0,i,k,j,0,o]
+  pp.alpha[t] = a;
+  pp.coef[t] = a * mk;
+  const int lo = -g.psmax - 1, hi = g.psmax + 1;
+  bool literal = false;
+  int thi = hi + 1, tlo = lo - 1, mlo = hi + 1, mhi = lo - 1;
+  if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
+    if (!(scales_ok(sw, sa) && a > 0.f && isfinite(a))) literal = true;
+  }
+  if (!literal) {
+    if (g.mode == ADC_TERNARY) {
+      thi = first_true_ternary_hi(lo, hi, sw, sa, a);
+      tlo = last_true_ternary_lo(lo, hi, sw, sa, a);
+    }
+    // STE interval: psb(p) monotone non-decreasing in p
+    {
+      int L = lo, R = hi + 1;  // first p with psb > thr_lo  (i.e. not "<= thr_lo")
+      while (L < R) {
+        int mid = L + ((R - L) >> 1);
+        float b = psb_literal(mid, g.mode, sw, sa, a);
+        if (b > g.thr_lo) R = mid; else L = mid + 1;
+      }
+      mlo = L;
+      L = lo - 1; R = hi;  // last p with psb < thr_hi
+      while (L < R) {
+        int mid = L + ((R - L + 1) >> 1);
+        float b = psb_literal(mid, g.mode, sw, sa, a);
+        if (b < g.thr_hi) L = mid; else R = mid - 1;
+      }
+      mhi = L;
+    }
+  }
+  pp.thi[t] = thi;
+  pp.tlo[t] = tlo;
+  // STE interval as (lo, span): pass <=> (unsigned)(ps - lo) <= (unsigned)span
+  if (mhi >= mlo) { pp.mlo[t] = mlo; pp.mhi[t] = mhi - mlo; }
+  else { pp.mlo[t] = -(1 << 30); pp.mhi[t] = 0; }
+  return literal;
+}
+
 __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, const float* __restrict__ sw_p,
                                    const float* __restrict__ sa_p, const int8_t* __restrict__ bmask,
                                    Params pp) {
   const float sw = *sw_p, sa = *sa_p;
-  const int npar = g.T * g.nba * g.nbw * g.Opad;
-  const int nkj = g.nbw * g.nba;
-  const bool scales_ok = (sw * sa > 0.f) && isfinite(sw * sa) && isfinite(sw) && isfinite(sa);
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < npar + nkj; t += gridDim.x * blockDim.x) {
-    if (t >= npar) {  // per-(k,j) float coefficients
-      const int kj = t - npar, k = kj / g.nba, j = kj - k * g.nba;
-      const float mk = (float)bmask[k * g.nba + j];  // binary_mask[0,0,k,j,0,0]
-      pp.ckj[kj] = mk;
-      pp.ckj[nkj + kj] = mk * pow2f(-g.bsa * j);  // E weight: 2^-(bsa*j) * mask
-      pp.ckj[2 * nkj + kj] = mk * pow2f(-g.bsw * k);  // D weight: 2^-(bsw*k) * mask
-      continue;
-    }
-    int r = t;
-    const int o = r % g.Opad; r /= g.Opad;
-    const int k = r % g.nbw; r /= g.nbw;
-    const int j = r % g.nba;
-    const int i = r / g.nba;
-    const float mk = (float)bmask[k * g.nba + j];
-    float a = 1.f;
-    if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && alpha_q != nullptr && o < g.O)
-      a = alpha_q[((i * g.nbw + k) * g.nba + j) * g.O + o];  // alpha[0,i,k,j,0,o]
-    pp.alpha[t] = a;
-    pp.coef[t] = a * mk;
-    const int lo = -g.psmax - 1, hi = g.psmax + 1;
-    bool literal = false;
-    int thi = hi + 1, tlo = lo - 1, mlo = hi + 1, mhi = lo - 1;
-    if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
-      if (!(scales_ok && a > 0.f && isfinite(a))) literal = true;
-    }
-    if (!literal) {
-      if (g.mode == ADC_TERNARY) {
-        thi = first_true_ternary_hi(lo, hi, sw, sa, a);
-        tlo = last_true_ternary_lo(lo, hi, sw, sa, a);
-      }
-      // STE interval: psb(p) monotone non-decreasing in p
-      {
-        int L = lo, R = hi + 1;  // first p with psb > thr_lo  (i.e. not "<= thr_lo")
-        while (L < R) {
-          int mid = L + ((R - L) >> 1);
-          float b = psb_literal(mid, g.mode, sw, sa, a);
-          if (b > g.thr_lo) R = mid; else L = mid + 1;
-        }
-        mlo = L;
-        L = lo - 1; R = hi;  // last p with psb < thr_hi
-        while (L < R) {
-          int mid = L + ((R - L + 1) >> 1);
-          float b = psb_literal(mid, g.mode, sw, sa, a);
-          if (b < g.thr_hi) L = mid; else R = mid - 1;
-        }
-        mhi = L;
-      }
-    }
-    pp.thi[t] = thi;
-    pp.tlo[t] = tlo;
-    // STE interval as (lo, span): pass <=> (unsigned)(ps - lo) <= (unsigned)span
-    if (mhi >= mlo) { pp.mlo[t] = mlo; pp.mhi[t] = mhi - mlo; }
-    else { pp.mlo[t] = -(1 << 30); pp.mhi[t] = 0; }
-    if (literal) atomicOr(&pp.flags[0], 1);
-  }
+  const ASrc as{alpha_q, 0, 0.f, 0.f};
+  const int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
+    if (params_item(g, as, sw, sa, bmask, pp, t)) atomicOr(&pp.flags[0], 1);
 }
 
 // =========================================================================================

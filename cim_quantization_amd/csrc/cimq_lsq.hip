@@ -18,139 +18,200 @@ struct LsqArgs {
   int nalpha;            // numel(alpha_cim) = T*nbw*nba*O
 };
 
-// grad_scale(x, s) forward value: (x - x*s).detach() + x*s  (_quan_base.py grad_scale)
-__device__ inline float grad_scale_value(float x, float s) {
-  const float yg = x * s;
-  const float d = x - yg;
-  return d + yg;
-}
+// block-wide reductions: across the wave with lane shuffles, then across the (<= 16) waves
+// through LDS with one barrier.  red needs 4 * 16 floats.
+__device__ inline float nan_max(float a, float b) { return (a != a || b != b) ? (a + b) : fmaxf(a, b); }
+__device__ inline float nan_min(float a, float b) { return (a != a || b != b) ? (a + b) : fminf(a, b); }
 
-// round_pass(v) forward value: (v.round() - v).detach() + v
-__device__ inline float round_pass_value(float v) {
-  const float r = rintf(v);
-  return (r - v) + v;
-}
-
-// block-wide (1024 threads) reductions
-__device__ inline float block_reduce_max(float v, float* red) {
-  red[threadIdx.x] = v;
+// (max, min) with torch.max / torch.min's NaN propagation
+__device__ inline float2 block_max_min(float mx, float mn, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = nan_max(mx, __shfl_xor(mx, o));
+    mn = nan_min(mn, __shfl_xor(mn, o));
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * w] = mx;
+    red[2 * w + 1] = mn;
+  }
   __syncthreads();
-  for (int s = blockDim.x >> 1; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      const float a = red[threadIdx.x], b = red[threadIdx.x + s];
-      red[threadIdx.x] = (a != a || b != b) ? (a + b) : fmaxf(a, b);  // torch.max propagates NaN
+  float2 r = make_float2(red[0], red[1]);
+  for (int i = 1; i < nw; ++i) {
+    r.x = nan_max(r.x, red[2 * i]);
+    r.y = nan_min(r.y, red[2 * i + 1]);
+  }
+  __syncthreads();
+  return r;
+}
+
+__device__ inline float4 block_sum4(float4 v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v.x += __shfl_xor(v.x, o);
+    v.y += __shfl_xor(v.y, o);
+    v.z += __shfl_xor(v.z, o);
+    v.w += __shfl_xor(v.w, o);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) reinterpret_cast<float4*>(red)[w] = v;
+  __syncthreads();
+  float4 r = reinterpret_cast<const float4*>(red)[0];
+  for (int i = 1; i < nw; ++i) {
+    const float4 t = reinterpret_cast<const float4*>(red)[i];
+    r.x += t.x;
+    r.y += t.y;
+    r.z += t.z;
+    r.w += t.w;
+  }
+  __syncthreads();
+  return r;
+}
+
+// =========================================================================================
+// forward prologue of the module entry points: one launch does the activation quantiser and
+// its slicing (the last nact_blocks blocks) and, in the first blocks, the weight quantiser
+// feeding every weight operand layout, alpha_cim's quantiser feeding the ADC thresholds, and
+// the scalars the later kernels read (one designated block).  Nothing is materialised in
+// between: each thread evaluates w_q / alpha_q for the elements it packs.
+// =========================================================================================
+struct ModulePrep {
+  const float* x;
+  const float* alpha_act;
+  const float* alpha_w;
+  const float* weight;
+  const float* alpha_cim;
+  const float* signed_act;
+  const int8_t* bmask;
+  uint8_t* xcf;
+  uint8_t* xcb;
+  v4i* wfrag;
+  v4i* wgx;   // general-kernel grad_x operand (nwg == 0 on the fast path)
+  uint4* wtc; // fast grad_x operand (nwt == 0 on the general path)
+  int Cp;
+  Params pp;
+  float* scal;  // [0] sa, [1] sw, [2] alpha scale, [3] max(alpha_cim), [4] min(alpha_cim)
+  int nact_blocks;
+  int nwf, nwg, nwt, npp;  // items of the weight-side roles
+};
+
+__global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, ModulePrep a) {
+  __shared__ float4 red4[16];
+  float* red = reinterpret_cast<float*>(red4);
+  const float sa = grad_scale_value(a.alpha_act[0], q.gs_a);  // lsq.py:547-548
+  // the few weight-side blocks go first so their latency-bound work overlaps the act stream
+  const int nwblk = (int)gridDim.x - a.nact_blocks;
+  if ((int)blockIdx.x >= nwblk) {
+    const int ab = (int)blockIdx.x - nwblk;
+    const bool sgn = a.signed_act[0] != 0.f;
+    const long long step = (long long)a.nact_blocks * blockDim.x;
+    for (long long idx = (long long)ab * blockDim.x + threadIdx.x; idx < g.Nin; idx += step)
+      act_item(g, a.x, sa, sgn, a.xcf, a.xcb, idx);
+    return;
+  }
+  const float sw = grad_scale_value(a.alpha_w[0], q.gs_w);  // lsq.py:553-554
+  ASrc as{nullptr, 1, 0.f, 0.f};
+  float mx = 0.f, mn = 0.f;
+  if (q.nbits_alpha > 0) {  // lsq.py:566-571
+    mx = -INFINITY;
+    mn = INFINITY;
+    for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
+      const float v = a.alpha_cim[e];
+      mx = (v != v || mx != mx) ? v + mx : fmaxf(mx, v);
+      mn = (v != v || mn != mn) ? v + mn : fminf(mn, v);
     }
-    __syncthreads();
+    const float2 r = block_max_min(mx, mn, red);
+    mx = r.x;
+    mn = r.y;
+    as.a = a.alpha_cim;
+    as.scale = (mx - mn) / (float)((1 << q.nbits_alpha) - 2);
+    as.qp_al = (float)((1 << q.nbits_alpha) - 1);
   }
-  const float r = red[0];
-  __syncthreads();
-  return r;
-}
-__device__ inline float block_reduce_min(float v, float* red) {
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int s = blockDim.x >> 1; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      const float a = red[threadIdx.x], b = red[threadIdx.x + s];
-      red[threadIdx.x] = (a != a || b != b) ? (a + b) : fminf(a, b);
+  const WSrc ws{a.weight, sw, 1, q.qn_w, q.qp_w};  // lsq.py:555
+  const int wb = (int)blockIdx.x;
+  if (wb == 0) {
+    // literal-ADC flag: any entry whose alpha_q / scales break the threshold search
+    bool lit = false;
+    if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
+      lit = !scales_ok(sw, sa);
+      if (as.a)
+        for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
+          const float v = as.get(e);
+          lit = lit || !(v > 0.f && isfinite(v));
+        }
     }
-    __syncthreads();
+    lit = __syncthreads_or(lit);
+    if (threadIdx.x == 0) {
+      a.scal[0] = sa;
+      a.scal[1] = sw;
+      a.scal[2] = as.scale;
+      a.scal[3] = mx;
+      a.scal[4] = mn;
+      a.pp.flags[0] = lit ? 1 : 0;
+      a.pp.flags[1] = a.pp.flags[2] = a.pp.flags[3] = 0;
+    }
   }
-  const float r = red[0];
-  __syncthreads();
-  return r;
-}
-__device__ inline float block_reduce_sum(float v, float* red) {
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int s = blockDim.x >> 1; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  const float r = red[0];
-  __syncthreads();
-  return r;
-}
-
-// One block of 1024 threads.  scal[0] = sa, scal[1] = sw, scal[2] = alpha scale,
-// scal[3] = max(alpha_cim), scal[4] = min(alpha_cim).
-__global__ __launch_bounds__(1024) void prep_lsq_kernel(Geo g, LsqArgs q, const float* __restrict__ alpha_act,
-                                                        const float* __restrict__ alpha_w,
-                                                        const float* __restrict__ weight,
-                                                        const float* __restrict__ alpha_cim,
-                                                        float* __restrict__ scal, float* __restrict__ wq,
-                                                        float* __restrict__ alpha_q) {
-  __shared__ float red[1024];
-  const float sa = grad_scale_value(alpha_act[0], q.gs_a);  // lsq.py:547-548
-  const float sw = grad_scale_value(alpha_w[0], q.gs_w);    // lsq.py:553-554
-  const int nw = g.O * g.K;
-  for (int e = threadIdx.x; e < nw; e += blockDim.x) {  // lsq.py:555
-    const float t = weight[e] / sw;
-    const float c = clamp_nan(t, q.qn_w, q.qp_w);
-    wq[e] = round_pass_value(c) * sw;
-  }
-  if (threadIdx.x == 0) {
-    scal[0] = sa;
-    scal[1] = sw;
-  }
-  if (q.nbits_alpha <= 0) return;
-  // lsq.py:566-571
-  float mx = -INFINITY, mn = INFINITY;
-  for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float a = alpha_cim[e];
-    mx = (a != a || mx != mx) ? a + mx : fmaxf(mx, a);
-    mn = (a != a || mn != mn) ? a + mn : fminf(mn, a);
-  }
-  mx = block_reduce_max(mx, red);
-  mn = block_reduce_min(mn, red);
-  const float qp_al = (float)((1 << q.nbits_alpha) - 1);
-  const float scale = (mx - mn) / (float)((1 << q.nbits_alpha) - 2);
-  for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float t = alpha_cim[e] / scale;
-    const float c = clamp_nan(round_pass_value(t), 1.f, qp_al);
-    alpha_q[e] = c * scale;
-  }
-  if (threadIdx.x == 0) {
-    scal[2] = scale;
-    scal[3] = mx;
-    scal[4] = mn;
+  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwt, total = e3 + a.npp;
+  for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
+    if (t < e1) wfrag_item(g, ws, a.wfrag, t);
+    else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
+    else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);
+    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e3);
   }
 }
 
-// grad_w reducer fused with the weight quantiser's backward: slab sum -> G = d loss / d w_q,
-// then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
-//   grad_weight = mask * (G * sw) / sw; partial sums of G * rp (MulBackward, d/d sw) and of
-//   -grad_t1 * ((w / sw) / sw) (DivBackward wrt the divisor) per block -> wpart[2*block].
-__global__ __launch_bounds__(1024) void reduce_gw_lsq_kernel(Geo g, LsqArgs q, int nchunks,
-                                                             const float* __restrict__ gw_slab,
-                                                             const float* __restrict__ scal,
-                                                             const float* __restrict__ weight,
-                                                             float* __restrict__ grad_weight,
-                                                             float* __restrict__ wpart) {
-  __shared__ float red[1024];
+// =========================================================================================
+// backward epilogue of the module entry points: two launches.  Blocks [0, nwb) reduce the
+// grad_w slabs and run the weight quantiser's backward; blocks [nwb, nwb + nga) reduce the
+// grad_alpha slabs into d loss / d alpha_q; then one block runs alpha_cim's quantiser
+// backward and the two step-size gradients.  With accum set, every parameter gradient is
+// added into its output buffer (torch's AccumulateGrad: grad = grad + new).
+// =========================================================================================
+struct ModuleTail {
+  const float* gw_slab;
+  const float* ga_slab;
+  const float* scal;
+  const float* weight;
+  const float* alpha_cim;
+  const float* apart;  // act-LSQ partials of the grad_x kernel
+  float* wpart;        // [2 * nwb] weight-LSQ partials
+  float* gaq;          // d loss / d alpha_q
+  float* grad_weight;
+  float* grad_alpha_act;
+  float* grad_alpha_w;
+  float* grad_alpha_cim;
+  Params pp;
+  float cgrad;  // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
+  int nchunks, nwb, nga, napart, accum;
+};
+
+// grad_w slab sum -> G = d loss / d w_q, then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
+//   grad_weight = mask * (G * sw) / sw; per block the partial sums of G * rp (MulBackward,
+//   d/d sw) and of -grad_t1 * ((w / sw) / sw) (DivBackward wrt the divisor) -> wpart[2*blk].
+__device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const size_t rows = (size_t)g.T * g.FBT * 16;
   const size_t nout = rows * g.Opad;
-  const size_t idx = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
   const int sub = threadIdx.x >> 6;
-  const float vsum = reduce_chunks(gw_slab, nout, nchunks, idx < nout ? idx : 0, red);
+  const float vsum = reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
   float p_mul = 0.f, p_div = 0.f;
   if (sub == 0 && idx < nout) {
-    const float v = vsum;
     const int o = (int)(idx % g.Opad);
     const size_t row = idx / g.Opad;
     const int i = (int)(row / (g.FBT * 16)), fl = (int)(row - (size_t)i * g.FBT * 16);
     const int f = i * g.xbar + fl;
     if (o < g.O && fl < g.xbar && f < g.K) {
-      const float sa = scal[0], sw = scal[1];
-      const float G = v * (sa / (float)g.nbw);  // d loss / d w_q (as reduce_gw_v3)
-      const float w = weight[(size_t)o * g.K + f];
-      const float t1 = w / sw;
+      const float sa = a.scal[0], sw = a.scal[1];
+      const float G = vsum * (sa / (float)g.nbw);  // d loss / d w_q (as reduce_gw_v3)
+      const size_t e = (size_t)o * g.K + f;
+      const float t1 = a.weight[e] / sw;
       const float c = clamp_nan(t1, q.qn_w, q.qp_w);
       const float rp = round_pass_value(c);
       const float grad_rp = G * sw;
       const bool pass = (t1 >= q.qn_w) && (t1 <= q.qp_w);
       const float grad_t1 = pass ? grad_rp : 0.f;
-      grad_weight[(size_t)o * g.K + f] = grad_t1 / sw;
+      const float gwv = grad_t1 / sw;
+      a.grad_weight[e] = a.accum ? a.grad_weight[e] + gwv : gwv;
       p_mul = G * rp;
       p_div = -grad_t1 * (t1 / sw);
     }
@@ -159,85 +220,118 @@ __global__ __launch_bounds__(1024) void reduce_gw_lsq_kernel(Geo g, LsqArgs q, i
   red[threadIdx.x] = p_mul;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float a = 0.f;
-    for (int t = 0; t < 64; ++t) a += red[t];
-    wpart[2 * blockIdx.x] = a;
+    float s = 0.f;
+    for (int t = 0; t < 64; ++t) s += red[t];
+    a.wpart[2 * blk] = s;
   }
   __syncthreads();
   red[threadIdx.x] = p_div;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float a = 0.f;
-    for (int t = 0; t < 64; ++t) a += red[t];
-    wpart[2 * blockIdx.x + 1] = a;
+    float s = 0.f;
+    for (int t = 0; t < 64; ++t) s += red[t];
+    a.wpart[2 * blk + 1] = s;
   }
 }
 
-// d loss / d alpha_weight = (sum G*rp + sum div-term) * gs_w  (GradScale's MulBackward);
-// d loss / d alpha_act = (sum of the act-LSQ partials) * gs_a.  One block of 1024 threads.
-__global__ __launch_bounds__(1024) void lsq_scalars_finish_kernel(LsqArgs q, int nw, const float* __restrict__ wpart,
-                                                                  int na, const float* __restrict__ apart,
-                                                                  float* __restrict__ grad_alpha_w,
-                                                                  float* __restrict__ grad_alpha_act) {
-  __shared__ float red[1024];
-  float m = 0.f, d = 0.f, a = 0.f;
-  for (int t = threadIdx.x; t < nw; t += blockDim.x) {
-    m += wpart[2 * t];
-    d += wpart[2 * t + 1];
-  }
-  for (int t = threadIdx.x; t < na; t += blockDim.x) a += apart[t];
-  m = block_reduce_sum(m, red);
-  d = block_reduce_sum(d, red);
-  a = block_reduce_sum(a, red);
-  if (threadIdx.x == 0) {
-    const float gsw = m + d;  // MulBackward's contribution reaches sw first, then DivBackward's
-    grad_alpha_w[0] = gsw * q.gs_w;
-    grad_alpha_act[0] = a * q.gs_a;
+__device__ inline void galpha_role(const Geo& g, const ModuleTail& a, int blk, float* red) {
+  const int nkj = g.nbw * g.nba;
+  const size_t nout = (size_t)g.T * nkj * g.Opad;
+  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
+  const float s = reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+  if ((threadIdx.x >> 6) == 0 && idx < nout) {
+    const int o = (int)(idx % g.Opad);
+    const size_t qq = idx / g.Opad;  // (i, k, j)
+    if (o < g.O) {
+      const int kj = (int)(qq % nkj);
+      const int i = (int)(qq / nkj);
+      const int k = kj / g.nba, j = kj - k * g.nba;
+      a.gaq[(((size_t)i * g.nbw + k) * g.nba + j) * g.O + o] = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
+    }
   }
 }
 
 // Backward of alpha_q = clamp(round_pass(a / scale), 1, qp) * scale, scale = (max - min) / N,
-// from G = d loss / d alpha_q.  One block of 1024 threads; ga[] = d loss / d alpha_cim.
-__global__ __launch_bounds__(1024) void alpha_cim_bwd_kernel(LsqArgs q, const float* __restrict__ alpha_cim,
-                                                             const float* __restrict__ scal,
-                                                             const float* __restrict__ G,
-                                                             float* __restrict__ ga) {
-  __shared__ float red[1024];
-  const float scale = scal[2], mx = scal[3], mn = scal[4];
+// from G = d loss / d alpha_q, as torch's engine runs it: DivBackward wrt a, then the scale's
+// MulBackward / DivBackward sums -> (max - min) / N -> MinBackward, then MaxBackward, each
+// spread evenly over ties.
+__device__ inline void alpha_cim_bwd_block(const LsqArgs& q, const ModuleTail& a, float* red) {
+  const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
   const float qp_al = (float)((1 << q.nbits_alpha) - 1);
   const float N = (float)((1 << q.nbits_alpha) - 2);
+  const float* G = a.gaq;
   float s_mul = 0.f, s_div = 0.f, cmax = 0.f, cmin = 0.f;
   for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float a = alpha_cim[e];
-    const float t = a / scale;
+    const float v = a.alpha_cim[e];
+    const float t = v / scale;
     const float rp = round_pass_value(t);
     const float c = clamp_nan(rp, 1.f, qp_al);
-    const float gc = G[e] * scale;
     const bool pass = (rp >= 1.f) && (rp <= qp_al);
-    const float gt = pass ? gc : 0.f;
-    ga[e] = gt / scale;  // DivBackward wrt a
+    const float gt = pass ? G[e] * scale : 0.f;
     s_mul += G[e] * c;
     s_div += -gt * (t / scale);
-    cmax += ((mx != mx) ? (a != a) : (a == mx)) ? 1.f : 0.f;
-    cmin += ((mn != mn) ? (a != a) : (a == mn)) ? 1.f : 0.f;
+    cmax += ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f;
+    cmin += ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f;
   }
-  s_mul = block_reduce_sum(s_mul, red);
-  s_div = block_reduce_sum(s_div, red);
-  cmax = block_reduce_sum(cmax, red);
-  cmin = block_reduce_sum(cmin, red);
+  const float4 r = block_sum4(make_float4(s_mul, s_div, cmax, cmin), red);
+  s_mul = r.x;
+  s_div = r.y;
+  cmax = r.z;
+  cmin = r.w;
   const float gscale = s_mul + s_div;  // d loss / d scale
   const float gdiff = gscale / N;      // DivBackward of (max - min) / N
-  const float gmax = gdiff, gmin = -gdiff;
-  const float pmax = gmax / cmax, pmin = gmin / cmin;  // evenly distributed over ties
+  const float pmax = gdiff / cmax, pmin = -gdiff / cmin;
   for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float a = alpha_cim[e];
-    const bool ismin = (mn != mn) ? (a != a) : (a == mn);
-    const bool ismax = (mx != mx) ? (a != a) : (a == mx);
-    float v = ga[e];
-    v = v + (ismin ? pmin : 0.f);  // MinBackward reaches alpha_cim before MaxBackward
-    v = v + (ismax ? pmax : 0.f);
-    ga[e] = v;
+    const float v = a.alpha_cim[e];
+    const float t = v / scale;
+    const float rp = round_pass_value(t);
+    const bool pass = (rp >= 1.f) && (rp <= qp_al);
+    const float gt = pass ? G[e] * scale : 0.f;
+    const bool ismin = (mn != mn) ? (v != v) : (v == mn);
+    const bool ismax = (mx != mx) ? (v != v) : (v == mx);
+    float r = gt / scale;          // DivBackward wrt a
+    r = r + (ismin ? pmin : 0.f);  // MinBackward reaches alpha_cim before MaxBackward
+    r = r + (ismax ? pmax : 0.f);
+    a.grad_alpha_cim[e] = a.accum ? a.grad_alpha_cim[e] + r : r;
   }
+}
+
+// d loss / d alpha_weight = (sum G*rp + sum div-term) * gs_w  (GradScale's MulBackward);
+// d loss / d alpha_act = (sum of the act-LSQ partials) * gs_a.
+__device__ inline void lsq_finish_block(const LsqArgs& q, const ModuleTail& a, float* red) {
+  float m = 0.f, d = 0.f, s = 0.f;
+  for (int t = threadIdx.x; t < a.nwb; t += blockDim.x) {
+    m += a.wpart[2 * t];
+    d += a.wpart[2 * t + 1];
+  }
+  for (int t = threadIdx.x; t < a.napart; t += blockDim.x) s += a.apart[t];
+  const float4 r = block_sum4(make_float4(m, d, s, 0.f), red);
+  m = r.x;
+  d = r.y;
+  s = r.z;
+  if (threadIdx.x == 0) {
+    const float gw = (m + d) * q.gs_w;  // MulBackward's contribution reaches sw first, then DivBackward's
+    const float ga = s * q.gs_a;
+    a.grad_alpha_w[0] = a.accum ? a.grad_alpha_w[0] + gw : gw;
+    a.grad_alpha_act[0] = a.accum ? a.grad_alpha_act[0] + ga : ga;
+  }
+}
+
+__global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q, ModuleTail a) {
+  __shared__ float red[1024];
+  const int b = (int)blockIdx.x;
+  if (b < a.nwb) gw_lsq_role(g, q, a, b, red);
+  else galpha_role(g, a, b - a.nwb, red);
+}
+
+// One block: alpha_cim's quantiser backward and the two step-size gradients, from the
+// partials module_bwd_tail_kernel left (a kernel boundary orders them across the XCDs'
+// L2s, which a last-block-done ticket would have to buy with an L2 writeback per block).
+__global__ __launch_bounds__(1024) void module_bwd_finish_kernel(LsqArgs q, ModuleTail a) {
+  __shared__ float4 red4[16];
+  float* red = reinterpret_cast<float*>(red4);
+  if (q.nbits_alpha > 0) alpha_cim_bwd_block(q, a, red);
+  lsq_finish_block(q, a, red);
 }
 
 // layout changes for the general (non-fast-path) kernels in module mode

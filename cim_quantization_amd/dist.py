@@ -27,6 +27,17 @@ class GradBucket:
             off += p.numel()
         self.nbytes = n * 4
 
+    def own(self, modules):
+        """Let the CiM layers among ``modules`` add their parameter gradients into this bucket
+        inside libcimq (no per-parameter AccumulateGrad kernels).  Only for parameters whose
+        gradients the bucket exchanges itself: parameter hooks do not see those gradients."""
+        mine = {id(p) for p in self.params}
+        for m in modules:
+            if hasattr(m, "accumulate_grads_in_place"):
+                if all(id(p) in mine for p in m.parameters()):
+                    m.accumulate_grads_in_place = True
+        return self
+
     def exchange(self, group=None):
         """Average the bucket over the ranks of ``group`` (no-op for a single process)."""
         if dist.is_available() and dist.is_initialized():

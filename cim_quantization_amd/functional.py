@@ -166,11 +166,19 @@ def cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, pad
 class _CimModuleConv(torch.autograd.Function):
     """A whole Conv2dLSQCiM layer after its first-step init (lsq.py:544-581): the activation,
     weight and alpha_cim quantisers run inside libcimq on the raw parameters (no torch ops,
-    no materialised x_q / w_q / alpha_q tensors); returns the NCHW output."""
+    no materialised x_q / w_q / alpha_q tensors); returns the NCHW output.
+
+    With ``accumulate`` set, the backward adds the parameter gradients straight into the
+    parameters' existing ``.grad`` buffers inside the library (what torch's AccumulateGrad
+    would do, without its four extra add kernels) and returns None for them.  It does so only
+    when all four ``.grad`` buffers exist as contiguous fp32 device tensors; otherwise the
+    gradients are returned as usual.  Parameter hooks (e.g. DistributedDataParallel's) do not
+    fire for in-place accumulated gradients, so this is for callers that own the gradient
+    exchange, like ``dist.GradBucket``."""
 
     @staticmethod
     def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
-                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha):
+                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
@@ -201,7 +209,25 @@ class _CimModuleConv(torch.autograd.Function):
                    "cimq_module_forward")
         ctx.desc, ctx.lsq, ctx.sizes = desc, lsq, sizes
         ctx.bufs = (xc, wc, aa, aw, ac, bm, sg, cbuf)
+        ctx.params = (weight, alpha_act, alpha_weight, alpha_cim) if accumulate else None
         return out
+
+    @staticmethod
+    def _grad_targets(ctx):
+        """The parameters' .grad buffers when the backward may accumulate into them."""
+        if ctx.params is None:
+            return None
+        grads = []
+        for p in ctx.params:
+            if p is None:
+                grads.append(None)
+                continue
+            g = p.grad
+            if (g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device
+                    or g.shape != p.shape):
+                return None
+            grads.append(g)
+        return grads
 
     @staticmethod
     def backward(ctx, grad_output):
@@ -209,28 +235,39 @@ class _CimModuleConv(torch.autograd.Function):
         dev = xc.device
         g = grad_output.detach().to(torch.float32).contiguous()
         gx = torch.empty_like(xc)
-        gw = torch.empty_like(wc)
-        gaa = torch.empty(1, device=dev, dtype=torch.float32)
-        gaw = torch.empty(1, device=dev, dtype=torch.float32)
-        gac = None if ac is None else torch.empty_like(ac)
+        targets = _CimModuleConv._grad_targets(ctx)
+        lsq = ctx.lsq
+        if targets is not None:
+            gw, gaa, gaw, gac = targets
+            lsq = _lib.make_lsq_desc(lsq.qn_w, lsq.qp_w, lsq.gscale_a, lsq.gscale_w, lsq.nbits_alpha,
+                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS)
+        else:
+            gw = torch.empty_like(wc)
+            gaa = torch.empty(1, device=dev, dtype=torch.float32)
+            gaw = torch.empty(1, device=dev, dtype=torch.float32)
+            gac = None if ac is None else torch.empty_like(ac)
         ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
         lib = _lib.load()
-        _lib.check(lib.cimq_module_backward(ctx.desc, ctx.lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
+        _lib.check(lib.cimq_module_backward(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
                                             aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),
                                             bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(),
                                             gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
                                             None if gac is None else gac.data_ptr(), ws.data_ptr(), _stream()),
                    "cimq_module_backward")
-        return (gx, gw, gaa, gaw, gac) + (None,) * 12
+        if targets is not None:
+            return (gx,) + (None,) * 17
+        return (gx, gw, gaa, gaw, gac) + (None,) * 13
 
 
 def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
-                    dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha):
+                    dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha,
+                    accumulate=False):
     """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
-    the three step-size parameters (alpha_act and alpha_weight are 1-element tensors)."""
+    the three step-size parameters (alpha_act and alpha_weight are 1-element tensors).
+    ``accumulate``: see _CimModuleConv."""
     return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
                                 padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
-                                nbits_alpha)
+                                nbits_alpha, accumulate)
 
 
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 2
+#define CIMQ_ABI_VERSION 3
 
 /* status codes */
 #define CIMQ_OK 0
@@ -49,6 +49,11 @@ extern "C" {
 /* what ``x`` holds (cimq_conv_desc.input_kind) */
 #define CIMQ_INPUT_XQ 0     /* x is x_q, the quantised activation handed to the Function (lsq.py:92) */
 #define CIMQ_INPUT_RAW_LSQ 1 /* x is the raw activation; the LSQ act quantiser (lsq.py:547-549) is fused */
+
+/* cimq_lsq_desc.flags */
+#define CIMQ_LSQ_ACCUMULATE_GRADS 1 /* cimq_module_backward adds the parameter gradients into
+                                       grad_weight / grad_alpha_* (torch's AccumulateGrad,
+                                       grad = grad + new) instead of overwriting them */
 
 typedef struct cimq_conv_desc {
   int32_t batch, in_channels, in_h, in_w; /* B, C, H, W */
@@ -69,7 +74,8 @@ typedef struct cimq_lsq_desc {
   float gscale_a;           /* grad_scale factor of alpha_act: 1/sqrt(numel(x) * Qp_a) (lsq.py:547) */
   float gscale_w;           /* grad_scale factor of alpha_weight: 1/sqrt(numel(w) * Qp_w) (lsq.py:553) */
   int32_t nbits_alpha;      /* alpha_cim quantiser bits (lsq.py:566-571); ignored unless adc 1 / 1.5 */
-  int32_t reserved[3];
+  int32_t flags;            /* CIMQ_LSQ_* bits */
+  int32_t reserved[2];
 } cimq_lsq_desc;
 
 typedef struct cimq_sizes {
@@ -124,7 +130,9 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
 
 /* Backward of cimq_module_forward: from d loss / d out (NCHW) to the gradients of the raw
  * activation and of the four parameters (weight, alpha_act, alpha_weight, alpha_cim), through
- * the quantisers as torch's autograd differentiates them. */
+ * the quantisers as torch's autograd differentiates them.  With CIMQ_LSQ_ACCUMULATE_GRADS in
+ * q->flags the parameter gradients are added into the four grad buffers (grad_x is always
+ * overwritten).  ctx must come from cimq_module_forward. */
 int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out, const float* x,
                          const float* weight, const float* alpha_act, const float* alpha_weight,
                          const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,

@@ -89,3 +89,45 @@ def test_fused_module_output_is_nchw_contiguous(cuda_device):
     y = m(x)
     assert y.is_contiguous() and tuple(y.shape) == (cfg["B"], cfg["O"], cfg["H"], cfg["H"])
     assert np.isfinite(y.detach().cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("idx", [0, 3])
+def test_fused_module_accumulates_into_existing_grads(cuda_device, idx):
+    """accumulate_grads_in_place: the library adds into the existing .grad buffers as torch's
+    AccumulateGrad would (old + new, fp32), and falls back to returned gradients when a .grad
+    buffer is missing.  (grad_w sums in LDS with float atomics, so two backward passes may
+    differ in the last bits: compared at 1e-5 of the largest magnitude.)"""
+
+    def close(a, b):
+        return (a - b).abs().max() <= 1e-5 * max(float(b.abs().max()), 1e-30) + 1e-12
+
+    cfg = CASES[idx]
+    x = torch.randn(cfg["B"], cfg["C"], cfg["H"], cfg["H"], generator=torch.Generator().manual_seed(3)).relu()
+    x = x.to(cuda_device)
+    plain = _build(cfg, cuda_device, 11)
+    acc = _build(cfg, cuda_device, 11)
+    plain(x)  # first-step init, then share the state
+    acc.load_state_dict(plain.state_dict())
+    acc.accumulate_grads_in_place = True
+    for m in (plain, acc):
+        for p in m.parameters():
+            p.grad = None
+    gy = None
+    old = {n: torch.randn(p.shape, generator=torch.Generator().manual_seed(5)).to(cuda_device)
+           for n, p in acc.named_parameters()}
+    for n, p in acc.named_parameters():
+        p.grad = old[n].clone()
+    for m in (plain, acc):
+        y = m(x)
+        if gy is None:
+            gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).to(cuda_device)
+        y.backward(gy)
+    for n, p in plain.named_parameters():
+        q = dict(acc.named_parameters())[n]
+        assert close(q.grad, old[n] + p.grad), n
+    # a missing .grad: gradients come back through autograd as usual
+    for p in acc.parameters():
+        p.grad = None
+    acc(x).backward(gy)
+    for n, p in plain.named_parameters():
+        assert close(dict(acc.named_parameters())[n].grad, p.grad), n
