@@ -12,6 +12,7 @@
 
 #include "../../include/cimq.h"
 #include "cimq_kernels_v3.hip"
+#include "cimq_gx_v6.hip"
 #include "cimq_lsq.hip"
 
 using namespace cimq;
@@ -120,7 +121,7 @@ CtxLayout ctx_layout(const Geo& g) {
   L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
-  L.wtc = o; o = align256(o + (size_t)g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
+  L.wtc = o; o = align256(o + (size_t)g.T * g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
   L.thi = o; o = align256(o + npar * 4);
   L.tlo = o; o = align256(o + npar * 4);
   L.mlo = o; o = align256(o + npar * 4);
@@ -200,6 +201,7 @@ struct Plan3 {
   bool ok;
   V3 v;
   size_t lds_fwd, lds_gx, lds_gw, lds_init;
+  size_t lds_gx6;  // 0: cim_bwd_gx_v6_kernel does not apply
 };
 
 inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -243,6 +245,22 @@ Plan3 v3_plan(const Geo& g) {
   v.fwd_res = fwd_res <= 80 * 1024 ? 1 : 0;
   p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
   p.lds_gx = a16((size_t)3 * (v.NPB + 1) * 32 * 2) + a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + ckl + 64;
+  {
+    // v6: G rows at pitch 40, two W buffers of the tile's channel blocks, the band's grad_out
+    // slab, two state buffers
+    v.NCBT = 0;
+    for (int i = 0; i < g.T; ++i) {
+      const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
+      v.NCBT = std::max(v.NCBT, c1 / 16 - c0 / 16 + 1);
+    }
+    const size_t pq = (size_t)64 * (g.NBP == 4 ? 2 : 4);
+    const size_t l6 = a16((size_t)3 * (v.NPB + 1) * 40 * 2) + 2 * a16((size_t)g.KHW * v.NCBT * 16 * 64) +
+                      a16((size_t)g.O * v.NPB * 4) + 2 * a16((size_t)2 * (v.NPB / 4) * pq) + ckl + 64;
+    p.lds_gx6 = (g.O % 16 == 0 && l6 <= kLdsMax - 512) ? l6 : 0;
+#ifdef CIMQ_GX_V5
+    p.lds_gx6 = 0;
+#endif
+  }
   v.NCG = 0;
   for (int i = 0; i < g.T; ++i) {
     const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
@@ -352,7 +370,7 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
                        reinterpret_cast<v4i*>(ctx + L.wgx));
     const int Cp = (g.C + 15) / 16 * 16;
-    const int tw = g.KHW * Cp * g.NKS * 4;
+    const int tw = g.T * g.KHW * Cp * g.NKS * 4;
     hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
                        reinterpret_cast<uint4*>(ctx + L.wtc));
     CIMQ_TRY(check_hip("prep_wgx"));
@@ -461,9 +479,20 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     float* part = reinterpret_cast<float*>(ws + W.lsq_part);
     dim3 grid(g.B * p.v.nbands);
-    auto kern = cim_bwd_gx_v5_kernel<NBP, 2, true>;
-    if (p.v.NT <= 16) kern = lsq ? cim_bwd_gx_v5_kernel<NBP, 2, true> : cim_bwd_gx_v5_kernel<NBP, 2, false>;
-    else kern = lsq ? cim_bwd_gx_v5_kernel<NBP, 4, true> : cim_bwd_gx_v5_kernel<NBP, 4, false>;
+    const bool two = p.v.NT <= 16;
+    if (p.lds_gx6) {
+      auto kern = two ? (lsq ? cim_bwd_gx_v6_kernel<NBP, 2, true> : cim_bwd_gx_v6_kernel<NBP, 2, false>)
+                      : (lsq ? cim_bwd_gx_v6_kernel<NBP, 4, true> : cim_bwd_gx_v6_kernel<NBP, 4, false>);
+      CIMQ_TRY(set_lds(kern, p.lds_gx6));
+      const int slot = prof_begin(KID_BWD_GX, g, s);
+      hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx6, s, g, p.v, ctx + L.st,
+                         reinterpret_cast<const uint4*>(ctx + L.wtc), pp, sw, sa, gout, x, gx, part);
+      prof_end(slot, s);
+      *lsq_fused = lsq;
+      return check_hip("cim_bwd_gx_v6");
+    }
+    auto kern = two ? (lsq ? cim_bwd_gx_v5_kernel<NBP, 2, true> : cim_bwd_gx_v5_kernel<NBP, 2, false>)
+                    : (lsq ? cim_bwd_gx_v5_kernel<NBP, 4, true> : cim_bwd_gx_v5_kernel<NBP, 4, false>);
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_BWD_GX, g, s);
     hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx, s, g, p.v, ctx + L.st,
@@ -684,7 +713,7 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
     a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 256), 8192);
     a.nwf = g.T * g.KS * g.NBLK * 64;
     a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;  // general grad_x kernel operand
-    a.nwt = fast ? g.KHW * a.Cp * g.NKS * 4 : 0;  // fast grad_x kernel operand
+    a.nwt = fast ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // fast grad_x kernel operand
     a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
     const int nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.npp, 256), 1024));
     const int slot = prof_begin(KID_PREP_ACT, g, s);

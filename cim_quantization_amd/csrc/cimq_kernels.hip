@@ -160,19 +160,23 @@ __device__ inline void wgx_item(const Geo& g, const WSrc& ws, v4i* __restrict__ 
   wgx[t] = o;
 }
 
-// grad_x transposed-GEMM operand: int8(slice) as bf16 in [khw][c (Cp)][kappa (NKS*32)] order,
-// wtc row (khw, c) = weight row f = c*KHW + khw, so one 16-B piece holds 8 consecutive kappa.
+// grad_x transposed-GEMM operand: int8(slice) as bf16 in [i][khw][c (Cp)][kappa (NKS*32)] order,
+// one copy per tile i with the rows of other tiles zeroed, so a kernel stages a tile's rows
+// by plain copy.  Row (i, khw, c) = weight row f = c*KHW + khw; one 16-B piece holds 8
+// consecutive kappa.
 __device__ inline void wtc_item(const Geo& g, const WSrc& ws, int Cp, uint4* __restrict__ wtc, int t) {
   const int KAP = g.NKS * 32;
   const int piece = t % (KAP / 8), row = t / (KAP / 8);
-  const int khw = row / Cp, c = row - khw * Cp;
+  const int i = row / (g.KHW * Cp), rr = row - i * (g.KHW * Cp);
+  const int khw = rr / Cp, c = rr - khw * Cp;
   const int f = c * g.KHW + khw;
+  const bool in_tile = c < g.C && f >= i * g.xbar && f < min(g.K, (i + 1) * g.xbar);
   uint32_t wd[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int kap = piece * 8 + e;
     float val = 0.f;
-    if (c < g.C && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, ws, f, kap));
+    if (in_tile && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, ws, f, kap));
     wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
   }
   wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
@@ -197,7 +201,7 @@ __global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const floa
 __global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,
                                 uint4* __restrict__ wtc) {
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
-  const int total = g.KHW * Cp * (g.NKS * 32 / 8);
+  const int total = g.T * g.KHW * Cp * (g.NKS * 32 / 8);
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wtc_item(g, ws, Cp, wtc, t);
 }

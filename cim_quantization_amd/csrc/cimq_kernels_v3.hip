@@ -31,6 +31,7 @@ struct V3 {
   int fwd_res;     // forward: every tile's weights / thresholds resident in LDS
   int nmt;         // M / 64
   int NCG;         // grad_w: max input channels one tile touches
+  int NCBT;        // grad_x: max 16-channel blocks one tile touches
   int CB;          // grad_x: 16-channel blocks of the output tile grid (ceil(C/16))
   int NT;          // grad_x: max output tiles (16 positions x 16 channels) per band
 };
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(512, 2) void cim_bwd_gx_v5_kernel(Geo g, V3 v, cons
               const int f = c * g.KHW + khw;
               val[u] = make_uint4(0, 0, 0, 0);
               if (c < g.C && f >= i * g.xbar && f < min(g.K, (i + 1) * g.xbar))
-                val[u] = wtc[((size_t)row * g.NKS + kc) * 4 + q8];
+                val[u] = wtc[(((size_t)i * g.KHW * Cp + row) * g.NKS + kc) * 4 + q8];
               dst[u] = row * (WPB / 8) + q8;
             }
           }

@@ -20,6 +20,12 @@ sys.path.insert(0, REPO)
 # name -> preprocessor defines; kernels carry CIMQ_EXP_* knobs only while an experiment runs
 VARIANTS = {
     "base": [],
+    "gx_v5": ["CIMQ_GX_V5"],
+    "noA": ["CIMQ_EXP_NO_PHASEA"],
+    "noB": ["CIMQ_EXP_NO_PHASEB"],
+    "noW": ["CIMQ_EXP_NO_WSTAGE"],
+    "noDMA": ["CIMQ_EXP_NO_DMA"],
+    "noAB": ["CIMQ_EXP_NO_PHASEA", "CIMQ_EXP_NO_PHASEB"],
 }
 
 
