@@ -13,6 +13,7 @@
 #include "../../include/cimq.h"
 #include "cimq_kernels_v3.hip"
 #include "cimq_gx_v6.hip"
+#include "cimq_v7.hip"
 #include "cimq_lsq.hip"
 
 using namespace cimq;
@@ -108,7 +109,7 @@ int make_geo(const cimq_conv_desc* d, Geo* out) {
 }
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t total;
 };
@@ -122,6 +123,7 @@ CtxLayout ctx_layout(const Geo& g) {
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
   L.wtc = o; o = align256(o + (size_t)g.T * g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
+  L.wcy = o; o = align256(o + (size_t)g.T * 12 * g.NKS * 64 * 16);  // v8 grad_x operand (<= 12 blocks / tile)
   L.thi = o; o = align256(o + npar * 4);
   L.tlo = o; o = align256(o + npar * 4);
   L.mlo = o; o = align256(o + npar * 4);
@@ -131,7 +133,8 @@ CtxLayout ctx_layout(const Geo& g) {
   L.ckj = o; o = align256(o + 3 * 64 * 4);
   L.flags = o; o = align256(o + 16);
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
-  L.st = o; o = align256(o + (size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4));
+  // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
+  L.st = o; o = align256(o + std::max((size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4), (size_t)g.T * g.M * g.O * 4));
   L.lsq_scal = o; o = align256(o + 16 * 4);
   L.total = o;
   return L;
@@ -174,27 +177,6 @@ size_t lds_gw(const Geo& g) {
 const size_t kLdsMax = 160 * 1024;
 
 bool gx_lds_ok(const Geo& g) { return lds_tile(g) + sizeof(float) * g.C * g.HW <= kLdsMax - 1024; }
-
-struct WsLayout {
-  size_t gw_slab, ga_slab, lsq_part, gaq, wpart, bpo, total;
-  int rows, nchunks;
-};
-
-WsLayout ws_layout(const Geo& g) {
-  WsLayout W;
-  gw_chunks(g, &W.rows, &W.nchunks);
-  size_t o = 0;
-  W.gw_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.FBT * 16 * g.Opad);
-  W.ga_slab = o; o = align256(o + sizeof(float) * W.nchunks * g.T * g.nbw * g.nba * g.Opad);
-  W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * ((g.H + 7) / 8)));
-  // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
-  // a [B, P, O] staging copy of out / grad_out for the general kernels
-  W.gaq = o; o = align256(o + sizeof(float) * (size_t)g.T * g.nbw * g.nba * g.O);
-  W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
-  W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
-  W.total = o;
-  return W;
-}
 
 // ---- v3 fast path (whole-row 64-pixel tiles): patch geometry and LDS budgets ----
 struct Plan3 {
@@ -275,6 +257,94 @@ Plan3 v3_plan(const Geo& g) {
   const size_t lim = kLdsMax - 512;
   p.ok = p.lds_fwd <= lim && p.lds_gx <= lim && p.lds_gw <= lim;
   return p;
+}
+
+// ---- v7 backward (compact state words, unfolded grad_x, conv-style grad_w) ----
+struct Plan7 {
+  bool ok;
+  V7 v;
+  size_t lds_gx, lds_gw;
+  int pairs;
+};
+
+Plan7 v7_plan(const Geo& g) {
+  Plan7 p;
+  memset(&p, 0, sizeof(p));
+#ifdef CIMQ_NO_V7
+  return p;
+#endif
+  const Plan3 p3 = v3_plan(g);
+  if (!p3.ok || g.NBP != 4) return p;
+  if (!((g.nbw == 3 && g.nba == 3) || (g.nbw == 2 && g.nba == 2))) return p;  // instantiated slice pairs
+  if (g.O % 16 != 0 || !(g.OB16 == 1 || g.OB16 == 2 || g.OB16 == 4)) return p;
+  // 3x3, stride 1, pad 1 ("same" conv: every CiM conv of the CIFAR ResNets but the downsampling ones)
+  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1) return p;
+  if (g.Wo % 8 != 0 || (g.Wo & (g.Wo - 1)) != 0 || g.Wo > 64 || g.M % 128 != 0 || g.FBT > 8) return p;
+  V7& v = p.v;
+  if (g.P % 128 == 0) v.whole = 0;
+  else if (128 % g.P == 0) v.whole = 1;
+  else return p;
+  v.lw = p3.v.lw;
+  v.RB = std::min(g.H, 16);
+  v.nbands = (g.H + v.RB - 1) / v.RB;
+  v.FBX = g.FBT;
+  // grad_x v8: (c, kh)-row blocks per tile, ring of output rows
+  v.NCPBT = 0;
+  for (int i = 0; i < g.T; ++i) {
+    const int cplo = (i * g.xbar) / 3, cphi = (std::min(g.K, (i + 1) * g.xbar) - 1) / 3;
+    v.NCPBT = std::max(v.NCPBT, (cphi >> 2) - (cplo >> 2) + 1);
+  }
+  if (v.NCPBT > 12) return p;
+  v.SWD = std::min(16, g.Wo);
+  v.NSEG = g.Wo / v.SWD;
+  v.NRS = 64 / g.Wo;
+  if (v.NRS < 1) return p;
+  v.RSLOT = v.NRS + 2;
+  p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (v.SWD + 2) * 4) + 64 * 4 + 64;
+  // grad_w
+  v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
+  v.CPITCH = v.NSLOT * g.Wo + 8;
+  const size_t planes = (size_t)g.nba * g.KW * 16 * v.CPITCH * 2;
+  p.lds_gw = std::max(a16(planes), (size_t)9 * 256 * 4) + 64 * 4 + (size_t)3 * g.nbw * g.nba * 16 * 4;
+  p.pairs = ((g.C + 15) / 16) * g.OB16;
+  const int stages = g.M / 128;
+  const int want = std::max(1, 512 / p.pairs);
+  v.nstage = std::max(1, (stages + want - 1) / want);
+  v.nchunks = (stages + v.nstage - 1) / v.nstage;
+  // tiles touching one channel block (register arrays sized for 4)
+  for (int cb = 0; cb * 16 < g.C; ++cb) {
+    const int ilo = (cb * 16 * g.KHW) / g.xbar, ihi = (std::min(g.C, cb * 16 + 16) * g.KHW - 1) / g.xbar;
+    if (ihi - ilo + 1 > 3) return p;
+  }
+  const size_t lim = kLdsMax - 512;
+  p.ok = p.lds_gx <= lim && p.lds_gw <= lim;
+  return p;
+}
+
+struct WsLayout {
+  size_t gw_slab, ga_slab, lsq_part, gaq, wpart, bpo, total;
+  int rows, nchunks, nchunks_bwd;
+};
+
+WsLayout ws_layout(const Geo& g) {
+  WsLayout W;
+  gw_chunks(g, &W.rows, &W.nchunks);
+  // backward slabs: the v7 grad_w kernel's pixel chunks when it applies (the alpha_cim init
+  // kernel keeps gw_chunks' split: W.nchunks / W.rows)
+  const Plan7 p7 = v7_plan(g);
+  W.nchunks_bwd = p7.ok ? p7.v.nchunks : W.nchunks;
+  const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
+  size_t o = 0;
+  W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
+  W.ga_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad);
+  W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * ((g.H + 7) / 8)));  // >= B * v7 bands
+  // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
+  // a [B, P, O] staging copy of out / grad_out for the general kernels
+  W.gaq = o; o = align256(o + sizeof(float) * (size_t)g.T * g.nbw * g.nba * g.O);
+  W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
+  W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
+  W.total = o;
+  return W;
 }
 
 template <typename K>
@@ -374,6 +444,13 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
                        reinterpret_cast<uint4*>(ctx + L.wtc));
     CIMQ_TRY(check_hip("prep_wgx"));
+    const Plan7 p7 = v7_plan(g);
+    if (p7.ok) {
+      const int tc = g.T * p7.v.NCPBT * g.NKS * 64;
+      hipLaunchKernelGGL(prep_wcy_kernel, dim3(cdiv(tc, blk)), dim3(blk), 0, s, g, w_q, sw, p7.v.NCPBT,
+                         reinterpret_cast<v4i*>(ctx + L.wcy));
+      CIMQ_TRY(check_hip("prep_wcy"));
+    }
   }
   Params pp = params_of(g, ctx);
   if (need_params) {
@@ -390,7 +467,8 @@ template <int NBP, int KS>
 int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
                   hipStream_t s) {
   CtxLayout L = ctx_layout(g);
-  auto kern = cim_fwd_v3_kernel<NBP, KS>;
+  // compact state words when the v7 backward will read them
+  auto kern = v7_plan(g).ok ? cim_fwd_v3_kernel<NBP, KS, true> : cim_fwd_v3_kernel<NBP, KS, false>;
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
   dim3 grid(std::min(p.v.nmt, 2048), cdiv(g.OB16, 4));
   const int slot = prof_begin(KID_FWD, g, s);
@@ -525,10 +603,54 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
   return check_hip("scale");
 }
 
+template <int NBW, int NBA, int OBX>
+int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
+                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq) {
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  Params pp = params_of(g, const_cast<uint8_t*>(ctx));
+  const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
+  {
+    auto kern = lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false>;
+    CIMQ_TRY(set_lds(kern, p.lds_gx));
+    const int slot = prof_begin(KID_BWD_GX, g, s);
+    hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256), p.lds_gx, s, g, p.v, st,
+                       reinterpret_cast<const v4i*>(ctx + L.wcy), pp, sw, sa, gout, x, gx,
+                       reinterpret_cast<float*>(ws + W.lsq_part));
+    prof_end(slot, s);
+    CIMQ_TRY(check_hip("cim_bwd_gx_v8"));
+  }
+  {
+    auto kern = cim_bwd_gw_v7_kernel<NBW, NBA>;
+    CIMQ_TRY(set_lds(kern, p.lds_gw));
+    const int slot = prof_begin(KID_BWD_GW, g, s);
+    hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(256), p.lds_gw, s, g, p.v, st, ctx + L.xhat, pp,
+                       gout, reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
+    prof_end(slot, s);
+    CIMQ_TRY(check_hip("cim_bwd_gw_v7"));
+  }
+  return CIMQ_OK;
+}
+
+template <int NBW, int NBA>
+int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
+                const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq) {
+  if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+  if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+  return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+}
+
 template <int NBP, int FBMAX>
 int launch_bwd_all(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa,
                    const float* signed_act, const float* gout, const float* x, float* gx, uint8_t* ws,
                    hipStream_t s, bool* lsq_fused) {
+  const Plan7 p7 = v7_plan(g);
+  if (p7.ok) {
+    const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
+    *lsq_fused = lsq;
+    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+  }
   CIMQ_TRY((launch_gx<NBP, FBMAX>(g, ctx, sw, sa, gout, x, gx, ws, s, lsq_fused)));
   CIMQ_TRY((launch_gw<NBP, FBMAX, false>(g, ctx, sw, sa, signed_act, gout, ws, s)));
   return CIMQ_OK;
@@ -552,7 +674,7 @@ int launch_reduce_galpha(const Geo& g, const uint8_t* ctx, uint8_t* ws, float cg
                          const float* sa, float* out, hipStream_t s) {
   WsLayout W = ws_layout(g);
   const long long nout = (long long)g.T * g.nbw * g.nba * g.Opad;
-  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks,
+  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, init ? W.nchunks : W.nchunks_bwd,
                      reinterpret_cast<const float*>(ws + W.ga_slab), params_of(g, const_cast<uint8_t*>(ctx)),
                      cgrad, init, sw, sa, (float)((double)g.B * g.P), (float)sqrt((double)g.qp), out);
   return check_hip("reduce_galpha");
@@ -631,7 +753,7 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   WsLayout W = ws_layout(g);
   {
     const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
-    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks,
+    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks_bwd,
                        reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
     CIMQ_TRY(check_hip("reduce_gw"));
   }
@@ -644,7 +766,8 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
     float* part = reinterpret_cast<float*>(w + W.lsq_part);
     int nparts;
     if (lsq_fused) {
-      nparts = g.B * v3_plan(g).v.nbands;
+      const Plan7 p7 = v7_plan(g);
+      nparts = g.B * (p7.ok ? p7.v.nbands : v3_plan(g).v.nbands);
     } else {
       int grid = cdiv(g.Nin, 256);
       if (grid > kLsqParts) grid = kLsqParts;
@@ -712,10 +835,14 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
     a.scal = scal;
     a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 256), 8192);
     a.nwf = g.T * g.KS * g.NBLK * 64;
-    a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;  // general grad_x kernel operand
-    a.nwt = fast ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // fast grad_x kernel operand
+    const Plan7 p7 = v7_plan(g);
+    a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;                   // general grad_x operand
+    a.nwt = (fast && !p7.ok) ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // v5 / v6 grad_x operand
+    a.wcy = reinterpret_cast<v4i*>(c + L.wcy);
+    a.ncpbt = p7.ok ? p7.v.NCPBT : 1;
+    a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;              // v8 grad_x operand
     a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-    const int nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.npp, 256), 1024));
+    const int nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, a);
     prof_end(slot, s);
@@ -781,7 +908,8 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
   if (lsq_fused) {
-    nparts = g.B * p.v.nbands;
+    const Plan7 p7 = v7_plan(g);
+    nparts = g.B * (p7.ok ? p7.v.nbands : p.v.nbands);
   } else {
     int grid = cdiv(g.Nin, 256);
     if (grid > kLsqParts) grid = kLsqParts;
@@ -805,7 +933,7 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
   a.grad_alpha_cim = grad_alpha_cim;
   a.pp = params_of(g, const_cast<uint8_t*>(c));
   a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
-  a.nchunks = W.nchunks;
+  a.nchunks = W.nchunks_bwd;
   a.nwb = cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64);
   a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
   a.napart = nparts;

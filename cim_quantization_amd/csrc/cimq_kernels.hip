@@ -160,6 +160,38 @@ __device__ inline void wgx_item(const Geo& g, const WSrc& ws, v4i* __restrict__ 
   wgx[t] = o;
 }
 
+// v8 grad_x operand (cimq_v7.hip): the same int8(slice) values as wgx with the MFMA rows
+// re-ordered so that row rho = 4*q + kw of cp-block cpb is weight row f = cp*KW + kw,
+// cp = cpb*4 + q = c*KH + kh (rho & 3 == 3 and rows outside tile i are zero): one lane of the
+// product then holds all KW taps of one (c, kh) for its pixel.  wcy[i][cb][s][lane][8 bf16],
+// cpb = cpb_lo(i) + cb, cpb_lo(i) = ((i*xbar) / KW) / 4, cb < ncpbt.
+__device__ inline void wcy_item(const Geo& g, const WSrc& ws, int ncpbt, v4i* __restrict__ wcy, int t) {
+  const int lane = t % WAVE;
+  int r = t / WAVE;
+  const int s = r % g.NKS;
+  r /= g.NKS;
+  const int cb = r % ncpbt;
+  const int i = r / ncpbt;
+  const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+  const int rho = lane & 15;
+  const int cp = ((flo / g.KW) / 4 + cb) * 4 + (rho >> 2), kw = rho & 3;
+  const int c = cp / g.KH, kh = cp - c * g.KH;
+  const int f = c * g.KHW + kh * g.KW + kw;
+  const bool ok = kw < g.KW && c < g.C && f >= flo && f < fhi;
+  uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int kb = 2 * s + (e >> 2);
+    const int kap = kb * 16 + 4 * (lane >> 4) + (e & 3);
+    float v = 0.f;
+    if (ok && kb < g.NBLK) v = (float)to_i8_wrap(wslice(g, ws, f, kap));
+    wd[e >> 1] |= (uint32_t)bf16_bits(v) << (16 * (e & 1));
+  }
+  v4i o;
+  o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
+  wcy[t] = o;
+}
+
 // grad_x transposed-GEMM operand: int8(slice) as bf16 in [i][khw][c (Cp)][kappa (NKS*32)] order,
 // one copy per tile i with the rows of other tiles zeroed, so a kernel stages a tile's rows
 // by plain copy.  Row (i, khw, c) = weight row f = c*KHW + khw; one 16-B piece holds 8
@@ -196,6 +228,14 @@ __global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const floa
   const int total = g.T * g.FBT * g.NKS * WAVE;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wgx_item(g, ws, wgx, t);
+}
+
+__global__ void prep_wcy_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int ncpbt,
+                                v4i* __restrict__ wcy) {
+  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
+  const int total = g.T * ncpbt * g.NKS * WAVE;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
+    wcy_item(g, ws, ncpbt, wcy, t);
 }
 
 __global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,

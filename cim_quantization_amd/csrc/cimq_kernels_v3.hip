@@ -276,7 +276,9 @@ __device__ inline uint32_t st_bits(bool pass, float code) {
   return (pass ? 1u : 0u) | ((code != 0.f) ? 2u : 0u) | ((code < 0.f) ? 4u : 0u);
 }
 
-template <int NBP, int KS>
+// CST: compact state words (cimq_v7.hip) -- one uint32 per (tile i, pixel m, channel o) at
+// st32[(i*M + m)*O + o], bits 3*(k*nba + j) + {0: STE pass, 1: code != 0, 2: code < 0}.
+template <int NBP, int KS, bool CST>
 __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
@@ -367,6 +369,11 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
       const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
+      uint32_t stc[4][4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) stc[a][c] = 0u;
       for (int k = 0; k < g.nbw; ++k) {
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
@@ -411,8 +418,12 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                 }
               }
             }
+            if (CST) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) stc[ob][r] |= stw[r] << (3 * g.nba * k);
+            }
             // state words of pixels wave*16 + 4*g4 + (0..3), channel o: one 4-pixel quad
-            if (o < g.O) {
+            if (!CST && o < g.O) {
               const size_t q = ((size_t)(i * g.nbw + k) * MQ + (size_t)mt * 16 + wave * 4 + g4) * g.O + o;
               if (sizeof(SW) == 2) {
                 reinterpret_cast<uint2*>(st)[q] = make_uint2(stw[0] | (stw[1] << 16), stw[2] | (stw[3] << 16));
@@ -420,6 +431,17 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                 reinterpret_cast<uint4*>(st)[q] = make_uint4(stw[0], stw[1], stw[2], stw[3]);
               }
             }
+          }
+        }
+      }
+      if (CST) {
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const int o = (og * 4 + ob) * 16 + r16;
+          if (ob < nob && o < g.O) {
+            uint32_t* s32 = reinterpret_cast<uint32_t*>(st) + ((size_t)i * g.M + (size_t)mt * 64 + wave * 16 + 4 * g4) * g.O + o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stc[ob][r];
           }
         }
       }

@@ -88,11 +88,12 @@ struct ModulePrep {
   v4i* wfrag;
   v4i* wgx;   // general-kernel grad_x operand (nwg == 0 on the fast path)
   uint4* wtc; // fast grad_x operand (nwt == 0 on the general path)
-  int Cp;
+  v4i* wcy;   // v8 grad_x operand (nwc == 0 unless the v7 backward applies)
+  int Cp, ncpbt;
   Params pp;
   float* scal;  // [0] sa, [1] sw, [2] alpha scale, [3] max(alpha_cim), [4] min(alpha_cim)
   int nact_blocks;
-  int nwf, nwg, nwt, npp;  // items of the weight-side roles
+  int nwf, nwg, nwt, nwc, npp;  // items of the weight-side roles
 };
 
 __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, ModulePrep a) {
@@ -151,12 +152,13 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
       a.pp.flags[1] = a.pp.flags[2] = a.pp.flags[3] = 0;
     }
   }
-  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwt, total = e3 + a.npp;
+  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwt, e4 = e3 + a.nwc, total = e4 + a.npp;
   for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
     if (t < e1) wfrag_item(g, ws, a.wfrag, t);
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);
-    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e3);
+    else if (t < e4) wcy_item(g, ws, a.ncpbt, a.wcy, t - e3);
+    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4);
   }
 }
 

@@ -1,0 +1,661 @@
+// cimq_v7.hip -- the backward of the CiM conv (lsq.py:244-386) from compact state words.
+//
+// The forward (cim_fwd_v3_kernel<.., CST = true>) leaves one uint32 per (tile i, output
+// pixel m, channel o): for every slice pair (k, j) the STE pass bit (lsq.py:310-313) and the
+// ADC code (lsq.py:321-332) of that partial sum, 3 bits at 3*(k*nba + j).  Two kernels
+// consume them:
+//
+//  * cim_bwd_gx_v7_kernel -- grad_x as the UNFOLDED product, then the nn.Fold adjoint in LDS:
+//      gx_unf[m, f] = sum_kappa W_i[f, kappa] * G_i[m, kappa],  kappa = (k, o),
+//      G_i[m, (k, o)] = g[m, o] * sum_j cE_kj * pass_ijk[m, o]       (cE = mask * 2^-bsa*j)
+//    on v_mfma_f32_16x16x32_bf16 with G split hi/mid/lo (fp32-exact products: W is a small
+//    integer).  The lane that reads the state words of pixel m (its MFMA column) for four
+//    consecutive channels IS the B-operand lane of (m, 8 kappa) -- G is built in registers,
+//    never staged.  Each 16 x 16 (f, m) result tile is added into an LDS image of the block's
+//    band of input rows (ds_add_f32: 16 consecutive columns x 4 kernel taps per
+//    instruction); the fused LSQ activation backward (lsq.py:549) reads the finished image.
+//    Only f-blocks that hold tile i's rows are multiplied (no tile-padding waste).
+//
+//  * cim_bwd_gw_v7_kernel -- grad_w (+ grad_alpha_cim partials) as a weight-gradient conv:
+//      gw[(c, kh, kw), o] = sum_j sum_m xhat_j[c, ih(m, kh), iw(m, kw)] * g[m, o] * D_ij[m, o]
+//    with D_ij = sum_k cD_kj * pass_ijk, i = tile of (c, kh, kw).  K = 32 output pixels per
+//    MFMA: the lane holding channel o and 8 consecutive pixels builds g * D_j in registers
+//    (B operand), and the activation slices come from LDS planes [j][kw][c][row][ow] that
+//    hold the kw-shifted (and stride-decimated) input rows, so every A fragment is one
+//    aligned 16-byte read.  grad_alpha partials sum code * g over the lane's 8 pixels.
+//
+// Both replace the state-word (16-bit per (i, k, quad, o)) kernels of cimq_kernels_v3.hip /
+// cimq_gx_v6.hip on layers the v7 plan accepts (host: v7_plan in cimq_api.hip).
+#pragma once
+#include "cimq_gx_v6.hip"
+
+namespace cimq {
+
+struct V7 {
+  int lw;       // log2(Wo)
+  // grad_x (v8: ring fold)
+  int NCPBT;    // (c, kh)-row blocks of 4 per tile (wcy operand)
+  int SWD;      // segment width: min(16, Wo) output columns per 16-lane MFMA column group
+  int NSEG;     // segments per output row
+  int NRS;      // output rows per step (64 pixels)
+  int RSLOT;    // ring rows (NRS + 2)
+  // grad_x
+  int RB;       // input rows owned by one block
+  int nbands;   // bands per image
+  int FBX;      // f-blocks per tile (FBT)
+  // grad_w
+  int NSLOT;    // staged input rows per 128-pixel stage
+  int CPITCH;   // plane channel pitch (bf16 elements)
+  int nstage;   // 128-pixel stages per chunk
+  int nchunks;  // pixel chunks
+  int whole;    // 1: a stage is 128/P whole images; 0: a stage is 128/Wo rows of one image
+};
+
+// pass-bit masks of the state word: all j of slice k / all k of slice j
+__host__ __device__ constexpr uint32_t pass_mask_k(int k, int nba) {
+  uint32_t m = 0;
+  for (int j = 0; j < nba; ++j) m |= 1u << (3 * (k * nba + j));
+  return m;
+}
+__host__ __device__ constexpr uint32_t pass_mask_j(int j, int nbw, int nba) {
+  uint32_t m = 0;
+  for (int k = 0; k < nbw; ++k) m |= 1u << (3 * (k * nba + j));
+  return m;
+}
+
+// lane l <- lane l+1 / l-1 of the same 16-lane row (0 past the row's end)
+__device__ inline float dpp_from_next(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, true));
+}
+__device__ inline float dpp_from_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, true));
+}
+
+// ---------------------------------------------------------------------------------------
+// grad_x, v8: unfolded product with the (c, kh, kw) rows ordered so that the nn.Fold adjoint
+// along kw is three DPP lane shifts, and along kh a pass over a ring of output rows in LDS.
+// stride 1, 3x3, pad 1 (v7_plan).  Block = image b, band of RB input rows; a step = 64 output
+// pixels (4 MFMA column groups, one per wave), NRS output rows.  Per step and tile i:
+//   y[(c, kh), iw] = sum_kw gx_unf[(c, kh, kw), ow = iw + 1 - kw]        (registers + DPP)
+// goes to ring[row][segment][(c, kh)][col]; after the step, the input rows whose three
+// contributing output rows are done are folded along kh, scaled, run through the LSQ act
+// backward and stored -- no atomics, every value written by exactly one lane.
+// ---------------------------------------------------------------------------------------
+template <int NBW, int NBA, int OBX, bool LSQ>
+__global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
+                                                            const v4i* __restrict__ wcy, Params pp,
+                                                            const float* __restrict__ sw_p,
+                                                            const float* __restrict__ sa_p,
+                                                            const float* __restrict__ gout,
+                                                            const float* __restrict__ x, float* __restrict__ gx,
+                                                            float* __restrict__ gsa_part) {
+  constexpr int NKS = (NBW * OBX + 1) / 2;
+  constexpr int NKJ = NBW * NBA;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
+  const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB);
+  const int oh_lo = max(0, r0 - 1), oh_hi = min(g.Ho - 1, r1);
+  const int nsteps = (oh_hi - oh_lo + v.NRS) / v.NRS;
+  const int CPP = g.C * 3;
+  const int RE = v.SWD + 2;
+  const int rrow = v.NSEG * CPP * RE;  // floats per ring row
+  float* ring = reinterpret_cast<float*>(smem);
+  float* cel = ring + (size_t)v.RSLOT * rrow;
+  float* red = cel + 64;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sw = *sw_p, sa = *sa_p;
+  const int Wo = 1 << v.lw;
+  for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cel[t] = pp.ckj[NKJ + t];
+  __syncthreads();
+  // nominal binary mask: cE_kj independent of j, so E_k = cE_k0 * popcount(pass bits of k)
+  bool nominal = true;
+  float cek[NBW];
+#pragma unroll
+  for (int k = 0; k < NBW; ++k) {
+    cek[k] = cel[k * NBA];
+#pragma unroll
+    for (int j = 1; j < NBA; ++j) nominal = nominal && (cel[k * NBA + j] == cek[k]);
+  }
+  const float scale = sw / (float)NBA;
+  float part = 0.f;
+  int done = r0 - 1;
+  for (int step = 0; step < nsteps; ++step) {
+    const int oh_s = oh_lo + step * v.NRS, oh_e = min(oh_hi, oh_s + v.NRS - 1);
+    const int q = 16 * wave + r16;
+    const int oh = oh_s + (q >> v.lw), ow = q & (Wo - 1);
+    const bool pv = oh <= oh_e;
+    const int pimg = (oh << v.lw) + ow;
+    const size_t m = (size_t)b * g.P + pimg;
+    const int seg = ow / v.SWD, col = ow - seg * v.SWD;
+    float* rr = ring + (size_t)((oh - oh_lo) % v.RSLOT) * rrow + seg * CPP * RE;
+    float gv[OBX][4];
+#pragma unroll
+    for (int ob = 0; ob < OBX; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = ob * 16 + 4 * g4 + r;
+        gv[ob][r] = pv ? (g.onchw ? gout[((size_t)b * g.O + o) * g.P + pimg] : gout[m * g.O + o]) : 0.f;
+      }
+    for (int i = 0; i < g.T; ++i) {
+      uint32_t sv[OBX][4];
+#pragma unroll
+      for (int ob = 0; ob < OBX; ++ob) {
+        uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
+        if (pv) s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + ob * 16 + 4 * g4);
+        sv[ob][0] = s4.x; sv[ob][1] = s4.y; sv[ob][2] = s4.z; sv[ob][3] = s4.w;
+      }
+      v8bf Gh[NKS], Gm[NKS], Gl[NKS];
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        float Gv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kb = 2 * s + (e >> 2), r = e & 3;
+          Gv[e] = 0.f;
+          if (kb < NBW * OBX) {
+            const int k = kb / OBX, ob = kb - k * OBX;
+            float E;
+            if (nominal) {
+              E = cek[k] * (float)__popc(sv[ob][r] & pass_mask_k(k, NBA));
+            } else {
+              E = 0.f;
+#pragma unroll
+              for (int j = 0; j < NBA; ++j) E += ((sv[ob][r] >> (3 * (k * NBA + j))) & 1u) ? cel[k * NBA + j] : 0.f;
+            }
+            Gv[e] = gv[ob][r] * E;
+          }
+        }
+        split3x8(Gv, Gh[s], Gm[s], Gl[s]);
+      }
+      const int cp_lo = (i * g.xbar) / 3, cp_hi = (min(g.K, (i + 1) * g.xbar) - 1) / 3;
+      const int cpb_lo = cp_lo >> 2, ncb = (cp_hi >> 2) - cpb_lo + 1;
+      const bool shared_first = i > 0 && cpb_lo == (((i * g.xbar - 1) / 3) >> 2);
+      const v4i* wt = wcy + (size_t)i * v.NCPBT * NKS * 64 + lane;
+#pragma unroll
+      for (int cb = 0; cb < 12; ++cb) {
+        if (cb < ncb) {
+          v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < NKS; ++s) {
+            const v8bf a = as_v8bf(wt[(cb * NKS + s) * 64]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gm[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gl[s], acc, 0, 0, 0);
+          }
+          // acc[kw] = gx_unf[(cp, kw)][this lane's pixel], cp = (cpb_lo + cb)*4 + g4
+          float fn = dpp_from_next(acc[0]);  // kw = 0 of pixel ow + 1 -> iw = ow
+          float fp = dpp_from_prev(acc[2]);  // kw = 2 of pixel ow - 1 -> iw = ow
+          if (col == v.SWD - 1) fn = 0.f;
+          if (col == 0) fp = 0.f;
+          const float y = (acc[1] + fn) + fp;
+          const int cp = (cpb_lo + cb) * 4 + g4;
+          if (pv && cp < CPP) {
+            float* e = rr + cp * RE;
+            if (cb == 0 && shared_first) {
+              e[col + 1] += y;
+              if (col == 0) e[0] += acc[0];
+              if (col == v.SWD - 1) e[v.SWD + 1] += acc[2];
+            } else {
+              e[col + 1] = y;
+              if (col == 0) e[0] = acc[0];
+              if (col == v.SWD - 1) e[v.SWD + 1] = acc[2];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // fold along kh the input rows whose contributing output rows are all in the ring
+    const int upto = (oh_e == g.Ho - 1) ? g.H - 1 : oh_e - 1;
+    const int f0 = max(done + 1, r0), f1 = min(upto, r1 - 1);
+    if (f1 >= f0) {
+      const int nf = (f1 - f0 + 1) * g.C * g.W;
+      for (int t = threadIdx.x; t < nf; t += blockDim.x) {
+        const int iw = t % g.W, rest = t / g.W;
+        const int c = rest % g.C, ih = f0 + rest / g.C;
+        const int sg = iw / v.SWD, cl = iw - sg * v.SWD;
+        float a = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const int oo = ih + 1 - kh;
+          if (oo >= oh_lo && oo <= oh_e) {
+            const float* e = ring + (size_t)((oo - oh_lo) % v.RSLOT) * rrow + (c * 3 + kh) * RE;
+            a += e[sg * CPP * RE + cl + 1];
+            if (cl == v.SWD - 1 && sg + 1 < v.NSEG) a += e[(sg + 1) * CPP * RE];
+            if (cl == 0 && sg > 0) a += e[(sg - 1) * CPP * RE + v.SWD + 1];
+          }
+        }
+        const size_t gi = (((size_t)b * g.C + c) * g.H + ih) * g.W + iw;
+        const float gqv = a * scale;
+        if (LSQ) {
+          // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v6_kernel
+          const float xv = x[gi];
+          const float y1 = xv / sa;
+          const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
+          const float rr2 = rintf(clv);
+          const float rp = (rr2 - clv) + clv;
+          const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
+          const float gy = pass ? gqv * sa : 0.f;
+          gx[gi] = gy / sa;
+          part += gqv * rp;
+          part += -(gy * (y1 / sa));
+        } else {
+          gx[gi] = gqv;
+        }
+      }
+      done = f1;
+    }
+    __syncthreads();
+  }
+  if (LSQ) {
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) red[wave] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) gsa_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// grad_x, v7 (kept for reference / experiments): LDS float-atomic fold
+// ---------------------------------------------------------------------------------------
+template <int NBW, int OBX, bool LSQ>
+__global__ __launch_bounds__(256, 2) void cim_bwd_gx_v7_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
+                                                            const v4i* __restrict__ wgx, Params pp,
+                                                            const float* __restrict__ sw_p,
+                                                            const float* __restrict__ sa_p,
+                                                            const float* __restrict__ gout,
+                                                            const float* __restrict__ x, float* __restrict__ gx,
+                                                            float* __restrict__ gsa_part) {
+  constexpr int NKS = (NBW * OBX + 1) / 2;  // 32-wide kappa chunks
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int nkj = NBW * g.nba;
+  const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
+  const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB), nrow = r1 - r0;
+  int oh_lo = r0 + g.PH - (g.KH - 1);
+  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.SH - 1) / g.SH;
+  const int oh_hi = min(g.Ho - 1, (r1 - 1 + g.PH) / g.SH);
+  const int npb = (oh_hi - oh_lo + 1) << v.lw;
+  const int ngrp = (npb + 15) >> 4;
+  const int RW = v.RB * g.W;
+
+  uint8_t* cur = smem;
+  float* gacc = reinterpret_cast<float*>(cur); cur += al16((size_t)g.C * RW * 4);
+  v4i* wfr = reinterpret_cast<v4i*>(cur); cur += (size_t)v.FBX * NKS * 64 * 16;
+  int* ftab = reinterpret_cast<int*>(cur); cur += (size_t)v.FBX * 16 * 4;
+  float* cel = reinterpret_cast<float*>(cur); cur += 64 * 4;
+  float* red = reinterpret_cast<float*>(cur);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sw = *sw_p, sa = *sa_p;
+  const int Wo = 1 << v.lw;
+
+  for (int t = threadIdx.x; t < g.C * RW; t += blockDim.x) gacc[t] = 0.f;
+  for (int t = threadIdx.x; t < nkj; t += blockDim.x) cel[t] = pp.ckj[nkj + t];
+
+  for (int i = 0; i < g.T; ++i) {
+    const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;
+    __syncthreads();
+    {
+      const v4i* src = wgx + (size_t)i * v.FBX * NKS * 64;
+      for (int t = threadIdx.x; t < fbn * NKS * 64; t += blockDim.x) wfr[t] = src[t];
+      for (int t = threadIdx.x; t < fbn * 16; t += blockDim.x) {
+        const int f = i * g.xbar + t;
+        int code = -1;
+        if (t < g.xbar && f < g.K) {
+          const int c = f / g.KHW, rem = f - c * g.KHW;
+          const int kh = rem / g.KW, kw = rem - kh * g.KW;
+          code = (c * RW) | (kh << 20) | (kw << 25);
+        }
+        ftab[t] = code;
+      }
+    }
+    __syncthreads();
+    for (int grp = wave; grp < ngrp; grp += 4) {
+      const int p = (grp << 4) + r16;  // band-relative output pixel = this lane's MFMA column
+      const bool pv = p < npb;
+      const int oh = oh_lo + (p >> v.lw), ow = p & (Wo - 1);
+      const int pimg = (oh << v.lw) + ow;
+      const size_t m = (size_t)b * g.P + pimg;
+      uint32_t sv[OBX][4];
+      float gv[OBX][4];
+#pragma unroll
+      for (int ob = 0; ob < OBX; ++ob) {
+        const int o0 = ob * 16 + 4 * g4;
+        if (pv) {
+          const uint4 s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + o0);
+          sv[ob][0] = s4.x; sv[ob][1] = s4.y; sv[ob][2] = s4.z; sv[ob][3] = s4.w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            gv[ob][r] = g.onchw ? gout[((size_t)b * g.O + o0 + r) * g.P + pimg] : gout[m * g.O + o0 + r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { sv[ob][r] = 0u; gv[ob][r] = 0.f; }
+        }
+      }
+      v4f acc[8];
+#pragma unroll
+      for (int fb = 0; fb < 8; ++fb) acc[fb] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        float G[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kb = 2 * s + (e >> 2), r = e & 3;
+          G[e] = 0.f;
+          if (kb < NBW * OBX) {
+            const int k = kb / OBX, ob = kb - k * OBX;
+            float E = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (j < g.nba) E += ((sv[ob][r] >> (3 * (k * g.nba + j))) & 1u) ? cel[k * g.nba + j] : 0.f;
+            G[e] = gv[ob][r] * E;
+          }
+        }
+        v8bf bh, bm, bl;
+        split3x8(G, bh, bm, bl);
+#pragma unroll
+        for (int fb = 0; fb < 8; ++fb) {
+          if (fb < fbn) {
+            const v8bf a = as_v8bf(wfr[(fb * NKS + s) * 64 + lane]);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
+          }
+        }
+      }
+      // nn.Fold adjoint: acc[fb][r] = gx_unf[f = fb*16 + 4*g4 + r][this lane's pixel]
+      if (pv) {
+        const int ihb = oh * g.SH - g.PH - r0, iwb = ow * g.SW - g.PW;
+#pragma unroll
+        for (int fb = 0; fb < 8; ++fb) {
+          if (fb < fbn) {
+            const int4 c4 = reinterpret_cast<const int4*>(ftab)[fb * 4 + g4];
+            const int cs[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int code = cs[r];
+              const int ih = ihb + ((code >> 20) & 31), iw = iwb + ((code >> 25) & 31);
+              if (code >= 0 && (unsigned)ih < (unsigned)nrow && (unsigned)iw < (unsigned)g.W)
+                atomicAdd(&gacc[(code & 0xFFFFF) + ih * g.W + iw], acc[fb][r]);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // epilogue: scale, fused LSQ activation backward (as cim_bwd_gx_v6_kernel), one store
+  const float scale = sw / (float)g.nba;
+  float part = 0.f;
+  const int nown = g.C * nrow * g.W;
+  for (int t = threadIdx.x; t < nown; t += blockDim.x) {
+    const int c = t / (nrow * g.W), q = t - c * (nrow * g.W);
+    const size_t gi = (((size_t)b * g.C + c) * g.H + r0) * g.W + q;
+    const float gqv = gacc[c * RW + q] * scale;
+    if (LSQ) {
+      const float xv = x[gi];
+      const float y1 = xv / sa;
+      const float cl = clamp_nan(y1, 0.f, g.lsq_qp);
+      const float rr2 = rintf(cl);
+      const float rp = (rr2 - cl) + cl;
+      const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
+      const float gy = pass ? gqv * sa : 0.f;
+      gx[gi] = gy / sa;
+      part += gqv * rp;
+      part += -(gy * (y1 / sa));
+    } else {
+      gx[gi] = gqv;
+    }
+  }
+  if (LSQ) {
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) red[wave] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) gsa_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// grad_w + grad_alpha_cim partials
+// ---------------------------------------------------------------------------------------
+// block = (pixel chunk, (channel block cb, output block ob)); a chunk is nstage stages of 128
+// output pixels; in a stage wave w owns the 32 pixels 32w..32w+31 (one MFMA K-step).
+// stride 1 (v7_plan); at most 3 crossbar tiles touch one 16-channel block.
+template <int NBW, int NBA>
+__global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
+                                                            const uint8_t* __restrict__ xcb, Params pp,
+                                                            const float* __restrict__ gout,
+                                                            float* __restrict__ gw_slab,
+                                                            float* __restrict__ ga_slab) {
+  constexpr int NKJ = NBW * NBA;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int chunk = blockIdx.x, pair = blockIdx.y;
+  const int cb = pair / g.OB16, ob = pair - cb * g.OB16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int Wo = 1 << v.lw;
+  const int KHW = g.KHW;
+  const int o = ob * 16 + r16;   // this lane's output channel (B column)
+  const int ca = cb * 16 + r16;  // this lane's input channel (A row)
+  // tiles touching this channel block; grad_alpha of tile i is owned by the block of the
+  // channel block holding the tile's first row
+  const int i_lo = (cb * 16 * KHW) / g.xbar;
+  const int i_hi = (min(g.C, cb * 16 + 16) * KHW - 1) / g.xbar;
+  const int ntl = i_hi - i_lo + 1;
+
+  const size_t plane = (size_t)16 * v.CPITCH;  // one (j, kw) plane, bf16 elements
+  uint8_t* cur = smem;
+  __bf16* pl = reinterpret_cast<__bf16*>(cur); { const size_t pb = (size_t)NBA * g.KW * plane * 2; cur += al16(pb > 9216 ? pb : (size_t)9216); }
+  float* cdl = reinterpret_cast<float*>(cur); cur += 64 * 4;
+  float* red = reinterpret_cast<float*>(cur);  // [3][NKJ][16] grad_alpha partials
+  for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
+  for (int t = threadIdx.x; t < 3 * NKJ * 16; t += blockDim.x) red[t] = 0.f;
+  __syncthreads();
+  // nominal binary mask: cD_kj independent of k, so D_j = cD_0j * popcount(pass bits of j)
+  bool nominal = true;
+  float cdj[NBA];
+#pragma unroll
+  for (int j = 0; j < NBA; ++j) {
+    cdj[j] = cdl[j];
+#pragma unroll
+    for (int k = 1; k < NBW; ++k) nominal = nominal && (cdl[k * NBA + j] == cdj[j]);
+  }
+
+  // per tap: tile of this lane's A row (-1: channel beyond C)
+  int tit[9];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp) tit[tp] = (tp < KHW && ca < g.C) ? (ca * KHW + tp) / g.xbar : -1;
+
+  v4f acc[9];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp) acc[tp] = v4f{0.f, 0.f, 0.f, 0.f};
+  float qs[3][NKJ];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < NKJ; ++c) qs[a][c] = 0.f;
+
+  for (int stg = 0; stg < v.nstage; ++stg) {
+    const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
+    const int b0 = (int)(m0 / g.P);
+    const int pim0 = (int)(m0 - (size_t)b0 * g.P);
+    const int oh0 = pim0 >> v.lw;
+    // staged rows: whole images b0.. (slot = (b - b0) * H + ih) or rows ih_first.. of b0
+    const int ih_first = v.whole ? 0 : oh0 - g.PH;
+    __syncthreads();
+    {
+      // item = (channel cl, slot, 8-column group): the 7 + KW source elements of the row
+      const int ng8 = Wo >> 3;
+      const int nit = 16 * v.NSLOT * ng8;
+      for (int it = threadIdx.x; it < nit; it += blockDim.x) {
+        const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
+        const int slot = rem / ng8, c8 = rem - slot * ng8;
+        int b = b0, ih = ih_first + slot;
+        if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
+        const int c = cb * 16 + cl;
+        const bool rowok = c < g.C && ih >= 0 && ih < g.H && b < g.B;
+        uint32_t wv[10];
+        const int iw0 = c8 * 8 - g.PW;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W;
+#pragma unroll
+        for (int u = 0; u < 10; ++u) {
+          const int iw = iw0 + u;
+          wv[u] = 0u;
+          if (u < 7 + g.KW && rowok && iw >= 0 && iw < g.W) wv[u] = src[iw];
+        }
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          if (kw < g.KW) {
+#pragma unroll
+            for (int j = 0; j < NBA; ++j) {
+              uint32_t pk[4];
+#pragma unroll
+              for (int e2 = 0; e2 < 4; ++e2) {
+                uint32_t h[2];
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                  const uint32_t w = wv[2 * e2 + h2 + kw];
+                  const float f = (float)(int8_t)((w >> (8 * j)) & 0xFFu);
+                  h[h2] = __float_as_uint(f) >> 16;  // small integers are exact in bf16
+                }
+                pk[e2] = h[0] | (h[1] << 16);
+              }
+              __bf16* dst = pl + ((size_t)(j * g.KW + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
+              *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // this wave's K-step: pixels mk .. mk+31; this lane's 8 pixels mk8 .. mk8+7 (one row)
+    const size_t mk8 = m0 + 32 * wave + 8 * g4;
+    if (mk8 >= (size_t)g.M) continue;
+    const int b = (int)(mk8 / g.P);
+    const int pimg = (int)(mk8 - (size_t)b * g.P);
+    const int oh = pimg >> v.lw, ow0 = pimg & (Wo - 1);
+    float gv[8];
+    if (g.onchw) {
+      const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
+      const float4 a0 = gp[0], a1 = gp[1];
+      gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
+      gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = gout[(mk8 + e) * g.O + o];
+    }
+    // row slot of each kernel row for this lane's output row (-1: outside the image)
+    int slot_kh[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh - g.PH + kh;
+      int sl = -1;
+      if (kh < g.KH && ih >= 0 && ih < g.H) sl = v.whole ? (b - b0) * g.H + ih : ih - ih_first;
+      slot_kh[kh] = sl;
+    }
+#pragma unroll
+    for (int tl = 0; tl < 3; ++tl) {
+      if (tl < ntl) {
+        const int i = i_lo + tl;
+        uint32_t sv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
+        // grad_alpha partials (lsq.py:321-333): sum over the pixels of code * g
+        if (((i * g.xbar) / KHW) / 16 == cb) {
+#pragma unroll
+          for (int kj = 0; kj < NKJ; ++kj) {
+            float q = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t bits = sv[e] >> (3 * kj);
+              const float t = (bits & 4u) ? -gv[e] : gv[e];
+              q += (bits & 2u) ? t : 0.f;
+            }
+            qs[tl][kj] += q;
+          }
+        }
+        // B operands: g * D_j, D_j = sum_k cD_kj * pass_ijk, split into bf16 hi / mid / lo
+        v8bf bh[NBA], bm[NBA], bq[NBA];
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) {
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float D;
+            if (nominal) {
+              D = cdj[j] * (float)__popc(sv[e] & pass_mask_j(j, NBW, NBA));
+            } else {
+              D = 0.f;
+#pragma unroll
+              for (int k = 0; k < NBW; ++k) D += ((sv[e] >> (3 * (k * NBA + j))) & 1u) ? cdl[k * NBA + j] : 0.f;
+            }
+            d[e] = gv[e] * D;
+          }
+          split3x8(d, bh[j], bm[j], bq[j]);
+        }
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          if (tp < KHW) {
+            const int kh = (g.KW == 3) ? tp / 3 : 0, kw = (g.KW == 3) ? tp - 3 * (tp / 3) : 0;
+            const int sl = slot_kh[kh];
+            const bool ok = (tit[tp] == i) && sl >= 0;
+            if (__any(ok)) {
+#pragma unroll
+              for (int j = 0; j < NBA; ++j) {
+                v4i av = {0, 0, 0, 0};
+                if (ok)
+                  av = *reinterpret_cast<const v4i*>(pl + ((size_t)(j * g.KW + kw) * 16 + r16) * v.CPITCH +
+                                                     sl * Wo + ow0);
+                const v8bf a = as_v8bf(av);
+                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
+                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
+                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  // reduce the four waves' partials in LDS (the planes are free now), write the slabs
+  __syncthreads();
+  float* gred = reinterpret_cast<float*>(pl);  // [9 taps][16 c][16 o]
+  for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) gred[t] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+    if (tp < KHW)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(&gred[(tp * 16 + 4 * g4 + r) * 16 + r16], acc[tp][r]);
+#pragma unroll
+  for (int tl = 0; tl < 3; ++tl)
+    if (tl < ntl)
+#pragma unroll
+      for (int kj = 0; kj < NKJ; ++kj) {
+        float q = qs[tl][kj];
+        q += __shfl_xor(q, 16);
+        q += __shfl_xor(q, 32);
+        if (g4 == 0) atomicAdd(&red[(tl * NKJ + kj) * 16 + r16], q);
+      }
+  __syncthreads();
+  const int FR = g.FBT * 16;
+  for (int t = threadIdx.x; t < KHW * 256; t += blockDim.x) {
+    const int tp = t >> 8, cr = (t >> 4) & 15, oc = t & 15;
+    const int c = cb * 16 + cr;
+    if (c < g.C) {
+      const int f = c * KHW + tp, i = f / g.xbar, fl = f - i * g.xbar;
+      gw_slab[(((size_t)chunk * g.T + i) * FR + fl) * g.Opad + ob * 16 + oc] = gred[(tp * 16 + cr) * 16 + oc];
+    }
+  }
+  for (int t = threadIdx.x; t < ntl * NKJ * 16; t += blockDim.x) {
+    const int tl = t / (NKJ * 16), rem = t - tl * NKJ * 16, kj = rem >> 4, oc = rem & 15;
+    const int i = i_lo + tl;
+    if (((i * g.xbar) / KHW) / 16 == cb)
+      ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + ob * 16 + oc] = red[t];
+  }
+}
+
+}  // namespace cimq
