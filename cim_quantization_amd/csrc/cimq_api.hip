@@ -39,6 +39,14 @@ int check_hip(const char* where) {
 }
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// tuning knobs for experiments (tools/): CIMQ_TUNE_<name>=<int> overrides a launch shape
+int tune(const char* name, int dflt) {
+  char key[64];
+  snprintf(key, sizeof(key), "CIMQ_TUNE_%s", name);
+  const char* v = getenv(key);
+  return v ? atoi(v) : dflt;
+}
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 int make_geo(const cimq_conv_desc* d, Geo* out) {
@@ -285,7 +293,7 @@ Plan7 v7_plan(const Geo& g) {
   else if (128 % g.P == 0) v.whole = 1;
   else return p;
   v.lw = p3.v.lw;
-  v.RB = std::min(g.H, 16);
+  v.RB = std::min(g.H, tune("GX_RB", 8));
   v.nbands = (g.H + v.RB - 1) / v.RB;
   v.FBX = g.FBT;
   // grad_x v8: (c, kh)-row blocks per tile, ring of output rows
@@ -305,10 +313,11 @@ Plan7 v7_plan(const Geo& g) {
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
   v.CPITCH = v.NSLOT * g.Wo + 8;
   const size_t planes = (size_t)g.nba * g.KW * 16 * v.CPITCH * 2;
-  p.lds_gw = std::max(a16(planes), (size_t)9 * 256 * 4) + 64 * 4 + (size_t)3 * g.nbw * g.nba * 16 * 4;
+  p.lds_gw = std::max(a16(planes), (size_t)4 * 9 * 256 * 4) + 64 * 4 + (size_t)4 * 3 * g.nbw * g.nba * 16 * 4;
+  if (16 * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
   p.pairs = ((g.C + 15) / 16) * g.OB16;
   const int stages = g.M / 128;
-  const int want = std::max(1, 512 / p.pairs);
+  const int want = std::max(1, tune("GW_BLOCKS", 512) / p.pairs);
   v.nstage = std::max(1, (stages + want - 1) / want);
   v.nchunks = (stages + v.nstage - 1) / v.nstage;
   // tiles touching one channel block (register arrays sized for 4)
@@ -337,7 +346,7 @@ WsLayout ws_layout(const Geo& g) {
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
   W.ga_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad);
-  W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * ((g.H + 7) / 8)));  // >= B * v7 bands
+  W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * g.H));  // >= B * bands
   // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
   // a [B, P, O] staging copy of out / grad_out for the general kernels
   W.gaq = o; o = align256(o + sizeof(float) * (size_t)g.T * g.nbw * g.nba * g.O);
@@ -470,7 +479,7 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   // compact state words when the v7 backward will read them
   auto kern = v7_plan(g).ok ? cim_fwd_v3_kernel<NBP, KS, true> : cim_fwd_v3_kernel<NBP, KS, false>;
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
-  dim3 grid(std::min(p.v.nmt, 2048), cdiv(g.OB16, 4));
+  dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, 4));
   const int slot = prof_begin(KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
                      reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);

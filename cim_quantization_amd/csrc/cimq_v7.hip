@@ -448,11 +448,10 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 
   const size_t plane = (size_t)16 * v.CPITCH;  // one (j, kw) plane, bf16 elements
   uint8_t* cur = smem;
-  __bf16* pl = reinterpret_cast<__bf16*>(cur); { const size_t pb = (size_t)NBA * g.KW * plane * 2; cur += al16(pb > 9216 ? pb : (size_t)9216); }
+  __bf16* pl = reinterpret_cast<__bf16*>(cur); { const size_t pb = (size_t)NBA * 3 * plane * 2; cur += al16(pb > 36864 ? pb : (size_t)36864); }
   float* cdl = reinterpret_cast<float*>(cur); cur += 64 * 4;
-  float* red = reinterpret_cast<float*>(cur);  // [3][NKJ][16] grad_alpha partials
+  float* red = reinterpret_cast<float*>(cur);  // [4 waves][3][NKJ][16] grad_alpha partials
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
-  for (int t = threadIdx.x; t < 3 * NKJ * 16; t += blockDim.x) red[t] = 0.f;
   __syncthreads();
   // nominal binary mask: cD_kj independent of k, so D_j = cD_0j * popcount(pass bits of j)
   bool nominal = true;
@@ -478,91 +477,134 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
     for (int c = 0; c < NKJ; ++c) qs[a][c] = 0.f;
 
-  for (int stg = 0; stg < v.nstage; ++stg) {
+  // Software pipeline over the chunk's stages: the global loads of stage n+1 (source words of
+  // the staged rows, state words and grad_out of this lane's K-step) are issued before the
+  // MFMA work of stage n, so their latency hides behind it.
+  const int ng8 = Wo >> 3;
+  const int nit = 16 * v.NSLOT * ng8;  // staging items (<= 2 per thread, v7_plan)
+  struct Pref {
+    uint32_t w[2][10];
+    uint32_t sv[3][8];
+    float gv[8];
+  };
+  auto stage_geom = [&](int stg, int& b0, int& ih_first) {
     const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
-    const int b0 = (int)(m0 / g.P);
+    b0 = (int)(m0 / g.P);
     const int pim0 = (int)(m0 - (size_t)b0 * g.P);
-    const int oh0 = pim0 >> v.lw;
-    // staged rows: whole images b0.. (slot = (b - b0) * H + ih) or rows ih_first.. of b0
-    const int ih_first = v.whole ? 0 : oh0 - g.PH;
-    __syncthreads();
-    {
-      // item = (channel cl, slot, 8-column group): the 7 + KW source elements of the row
-      const int ng8 = Wo >> 3;
-      const int nit = 16 * v.NSLOT * ng8;
-      for (int it = threadIdx.x; it < nit; it += blockDim.x) {
+    ih_first = v.whole ? 0 : (pim0 >> v.lw) - g.PH;
+  };
+  auto load = [&](int stg, Pref& pf) {
+    int b0, ih_first;
+    stage_geom(stg, b0, ih_first);
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2) {
+      const int it = threadIdx.x + u2 * 256;
+#pragma unroll
+      for (int u = 0; u < 10; ++u) pf.w[u2][u] = 0u;
+      if (it < nit) {
         const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
         const int slot = rem / ng8, c8 = rem - slot * ng8;
         int b = b0, ih = ih_first + slot;
         if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
         const int c = cb * 16 + cl;
-        const bool rowok = c < g.C && ih >= 0 && ih < g.H && b < g.B;
-        uint32_t wv[10];
-        const int iw0 = c8 * 8 - g.PW;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W;
-#pragma unroll
-        for (int u = 0; u < 10; ++u) {
-          const int iw = iw0 + u;
-          wv[u] = 0u;
-          if (u < 7 + g.KW && rowok && iw >= 0 && iw < g.W) wv[u] = src[iw];
+        if (c < g.C && ih >= 0 && ih < g.H && b < g.B) {
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 8;
+          const uint4 lo = reinterpret_cast<const uint4*>(src)[0], hi = reinterpret_cast<const uint4*>(src)[1];
+          pf.w[u2][1] = lo.x; pf.w[u2][2] = lo.y; pf.w[u2][3] = lo.z; pf.w[u2][4] = lo.w;
+          pf.w[u2][5] = hi.x; pf.w[u2][6] = hi.y; pf.w[u2][7] = hi.z; pf.w[u2][8] = hi.w;
+          if (c8 > 0) pf.w[u2][0] = src[-1];
+          if (c8 * 8 + 8 < g.W) pf.w[u2][9] = src[8];
         }
+      }
+    }
+    const size_t mk8 = ((size_t)chunk * v.nstage + stg) * 128 + 32 * wave + 8 * g4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pf.gv[e] = 0.f;
+#pragma unroll
+    for (int tl = 0; tl < 3; ++tl)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pf.sv[tl][e] = 0u;
+    if (mk8 < (size_t)g.M) {
+      const int b = (int)(mk8 / g.P);
+      const int pimg = (int)(mk8 - (size_t)b * g.P);
+      if (g.onchw) {
+        const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
+        const float4 a0 = gp[0], a1 = gp[1];
+        pf.gv[0] = a0.x; pf.gv[1] = a0.y; pf.gv[2] = a0.z; pf.gv[3] = a0.w;
+        pf.gv[4] = a1.x; pf.gv[5] = a1.y; pf.gv[6] = a1.z; pf.gv[7] = a1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pf.gv[e] = gout[(mk8 + e) * g.O + o];
+      }
+#pragma unroll
+      for (int tl = 0; tl < 3; ++tl)
+        if (tl < ntl)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pf.sv[tl][e] = st[((size_t)(i_lo + tl) * g.M + mk8 + e) * g.O + o];
+    }
+  };
+
+  Pref pf;
+  load(0, pf);
+  for (int stg = 0; stg < v.nstage; ++stg) {
+    int b0, ih_first;
+    stage_geom(stg, b0, ih_first);
+    __syncthreads();
+    // bf16 planes of the staged rows: item (channel cl, slot, 8-column group), kw shifts
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2) {
+      const int it = threadIdx.x + u2 * 256;
+      if (it < nit) {
+        const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
+        const int slot = rem / ng8, c8 = rem - slot * ng8;
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
-          if (kw < g.KW) {
 #pragma unroll
-            for (int j = 0; j < NBA; ++j) {
-              uint32_t pk[4];
+          for (int j = 0; j < NBA; ++j) {
+            uint32_t pk[4];
 #pragma unroll
-              for (int e2 = 0; e2 < 4; ++e2) {
-                uint32_t h[2];
-#pragma unroll
-                for (int h2 = 0; h2 < 2; ++h2) {
-                  const uint32_t w = wv[2 * e2 + h2 + kw];
-                  const float f = (float)(int8_t)((w >> (8 * j)) & 0xFFu);
-                  h[h2] = __float_as_uint(f) >> 16;  // small integers are exact in bf16
-                }
-                pk[e2] = h[0] | (h[1] << 16);
-              }
-              __bf16* dst = pl + ((size_t)(j * g.KW + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
-              *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const uint32_t w0 = pf.w[u2][2 * e2 + kw], w1 = pf.w[u2][2 * e2 + 1 + kw];
+              const float f0 = (float)(int8_t)((w0 >> (8 * j)) & 0xFFu);
+              const float f1 = (float)(int8_t)((w1 >> (8 * j)) & 0xFFu);
+              pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);  // exact bf16
             }
+            __bf16* dst = pl + ((size_t)(j * 3 + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
       }
     }
+    float gv[8];
+    uint32_t svc[3][8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = pf.gv[e];
+#pragma unroll
+    for (int tl = 0; tl < 3; ++tl)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) svc[tl][e] = pf.sv[tl][e];
     __syncthreads();
+    if (stg + 1 < v.nstage) load(stg + 1, pf);
     // this wave's K-step: pixels mk .. mk+31; this lane's 8 pixels mk8 .. mk8+7 (one row)
-    const size_t mk8 = m0 + 32 * wave + 8 * g4;
+    const size_t mk8 = ((size_t)chunk * v.nstage + stg) * 128 + 32 * wave + 8 * g4;
     if (mk8 >= (size_t)g.M) continue;
     const int b = (int)(mk8 / g.P);
     const int pimg = (int)(mk8 - (size_t)b * g.P);
     const int oh = pimg >> v.lw, ow0 = pimg & (Wo - 1);
-    float gv[8];
-    if (g.onchw) {
-      const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
-      const float4 a0 = gp[0], a1 = gp[1];
-      gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
-      gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gv[e] = gout[(mk8 + e) * g.O + o];
-    }
     // row slot of each kernel row for this lane's output row (-1: outside the image)
     int slot_kh[3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = oh - g.PH + kh;
       int sl = -1;
-      if (kh < g.KH && ih >= 0 && ih < g.H) sl = v.whole ? (b - b0) * g.H + ih : ih - ih_first;
+      if (ih >= 0 && ih < g.H) sl = v.whole ? (b - b0) * g.H + ih : ih - ih_first;
       slot_kh[kh] = sl;
     }
 #pragma unroll
     for (int tl = 0; tl < 3; ++tl) {
       if (tl < ntl) {
         const int i = i_lo + tl;
-        uint32_t sv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
+        const uint32_t* sv = svc[tl];
         // grad_alpha partials (lsq.py:321-333): sum over the pixels of code * g
         if (((i * g.xbar) / KHW) / 16 == cb) {
 #pragma unroll
@@ -598,38 +640,33 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         }
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
-          if (tp < KHW) {
-            const int kh = (g.KW == 3) ? tp / 3 : 0, kw = (g.KW == 3) ? tp - 3 * (tp / 3) : 0;
-            const int sl = slot_kh[kh];
-            const bool ok = (tit[tp] == i) && sl >= 0;
-            if (__any(ok)) {
+          const int kh = tp / 3, kw = tp - 3 * (tp / 3);
+          const int sl = slot_kh[kh];
+          const bool ok = (tit[tp] == i) && sl >= 0;
+          if (__any(ok)) {
 #pragma unroll
-              for (int j = 0; j < NBA; ++j) {
-                v4i av = {0, 0, 0, 0};
-                if (ok)
-                  av = *reinterpret_cast<const v4i*>(pl + ((size_t)(j * g.KW + kw) * 16 + r16) * v.CPITCH +
-                                                     sl * Wo + ow0);
-                const v8bf a = as_v8bf(av);
-                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
-                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
-                acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
-              }
+            for (int j = 0; j < NBA; ++j) {
+              v4i av = {0, 0, 0, 0};
+              if (ok)
+                av = *reinterpret_cast<const v4i*>(pl + ((size_t)(j * 3 + kw) * 16 + r16) * v.CPITCH + sl * Wo + ow0);
+              const v8bf a = as_v8bf(av);
+              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
+              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
+              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
             }
           }
         }
       }
     }
   }
-  // reduce the four waves' partials in LDS (the planes are free now), write the slabs
+  // reduce the four waves' partials through LDS (the planes are free now; plain stores, one
+  // region per wave -- LDS float atomics are slow), then write the slabs
   __syncthreads();
-  float* gred = reinterpret_cast<float*>(pl);  // [9 taps][16 c][16 o]
-  for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) gred[t] = 0.f;
-  __syncthreads();
+  float* gred = reinterpret_cast<float*>(pl);  // [4 waves][9 taps][16 c][16 o]
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp)
-    if (tp < KHW)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&gred[(tp * 16 + 4 * g4 + r) * 16 + r16], acc[tp][r]);
+    for (int r = 0; r < 4; ++r) gred[((wave * 9 + tp) * 16 + 4 * g4 + r) * 16 + r16] = acc[tp][r];
 #pragma unroll
   for (int tl = 0; tl < 3; ++tl)
     if (tl < ntl)
@@ -638,23 +675,27 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         float q = qs[tl][kj];
         q += __shfl_xor(q, 16);
         q += __shfl_xor(q, 32);
-        if (g4 == 0) atomicAdd(&red[(tl * NKJ + kj) * 16 + r16], q);
+        if (g4 == 0) red[((wave * 3 + tl) * NKJ + kj) * 16 + r16] = q;
       }
   __syncthreads();
   const int FR = g.FBT * 16;
-  for (int t = threadIdx.x; t < KHW * 256; t += blockDim.x) {
+  for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) {
     const int tp = t >> 8, cr = (t >> 4) & 15, oc = t & 15;
     const int c = cb * 16 + cr;
     if (c < g.C) {
       const int f = c * KHW + tp, i = f / g.xbar, fl = f - i * g.xbar;
-      gw_slab[(((size_t)chunk * g.T + i) * FR + fl) * g.Opad + ob * 16 + oc] = gred[(tp * 16 + cr) * 16 + oc];
+      const float sum = (gred[t] + gred[9 * 256 + t]) + (gred[2 * 9 * 256 + t] + gred[3 * 9 * 256 + t]);
+      gw_slab[(((size_t)chunk * g.T + i) * FR + fl) * g.Opad + ob * 16 + oc] = sum;
     }
   }
   for (int t = threadIdx.x; t < ntl * NKJ * 16; t += blockDim.x) {
     const int tl = t / (NKJ * 16), rem = t - tl * NKJ * 16, kj = rem >> 4, oc = rem & 15;
     const int i = i_lo + tl;
-    if (((i * g.xbar) / KHW) / 16 == cb)
-      ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + ob * 16 + oc] = red[t];
+    if (((i * g.xbar) / KHW) / 16 == cb) {
+      const int w1 = 3 * NKJ * 16;
+      const float sum = (red[t] + red[w1 + t]) + (red[2 * w1 + t] + red[3 * w1 + t]);
+      ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + ob * 16 + oc] = sum;
+    }
   }
 }
 
