@@ -36,7 +36,13 @@ RESNET20 += [(f"layer2.{b}.conv{c}", 32, 32, 16, 1, 3) for b in (1, 2) for c in 
 RESNET20 += [("layer3.0.conv1", 32, 64, 16, 2, 3), ("layer3.0.conv2", 64, 64, 8, 1, 3)]
 RESNET20 += [(f"layer3.{b}.conv{c}", 64, 64, 8, 1, 3) for b in (1, 2) for c in (1, 2)]
 XBAR, ADC = 128, 1.5
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward runs bf16 x3
+PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r01_v8", "pmc_traffic.json"))
+# rocprof symbol of each v7-path kernel id (the names pmc_traffic.json is keyed by)
+V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, true>", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
+              "gw_v7": "cimq::cim_bwd_gw_v7_kernel<3, 3>"}
 
 
 def out_hw(h, s):
@@ -208,13 +214,13 @@ def main():
         tr.step(xs, gs)
     torch.cuda.synchronize(dev)
 
-    # pick the dominant libcimq kernel from one untimed profiled step per kernel
+    # per-role kernel ms of one untimed step (all variants), and the dominant v7-path kernel
     per_kernel = {}
-    for kname in ("fwd", "bwd_gx", "bwd_gw", "prep_act"):
+    for kname in ("fwd", "bwd_gx", "bwd_gw", "prep_act", "fwd_v7", "gx_v8", "gw_v7"):
         with _lib.KernelTimer(kname) as kt:
             tr.step(xs, gs)
         per_kernel[kname] = kt.total_ms
-    dominant = max(per_kernel, key=per_kernel.get)
+    dominant = max(("fwd_v7", "gx_v8", "gw_v7"), key=per_kernel.get)
 
     graph = not args.no_graph
     if graph:
@@ -240,8 +246,31 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     macs_step = macs_per_sample() * args.batch * world
     value = macs_step / (elapsed / args.steps)
-    avg_launch_ms = kt.total_ms / max(kt.launches, 1)
-    achieved = (kt.algo_bytes / max(kt.launches, 1)) / (avg_launch_ms * 1e-3) / 1e9
+    nl = max(kt.launches, 1)
+    avg_launch_ms = kt.total_ms / nl
+    bytes_l, flops_l = kt.algo_bytes / nl, kt.algo_flops / nl
+    # both roofs of the kernel: HBM on the algorithmic bytes; MFMA on the
+    # algorithmic products as the kernel issues them (backward: fp32-accurate = 3 bf16 MFMAs;
+    # forward: nbw*nba = 9 int8 bit-slice products per logical MAC)
+    t_hbm = bytes_l / (PEAK_HBM_GBS * 1e9)
+    mfma_ops = flops_l * (9.0 if dominant == "fwd_v7" else 3.0)
+    mfma_peak = PEAK_I8_TOPS if dominant == "fwd_v7" else PEAK_BF16_TFLOPS
+    t_mfma = mfma_ops / (mfma_peak * 1e12)
+    traffic = None
+    if os.path.exists(TRAFFIC_JSON):
+        import json as _json
+        tj = _json.load(open(TRAFFIC_JSON))
+        hits = [v["traffic_bytes"] for k, v in tj.items() if k.startswith(V7_SYMBOLS[dominant])]
+        if hits:
+            traffic = sum(hits) / len(hits)
+    if t_hbm >= t_mfma:
+        roof = {"bound": "hbm", "achieved": bytes_l / (avg_launch_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+                "unit": "GB/s"}
+    else:
+        roof = {"bound": "mfma", "achieved": mfma_ops / (avg_launch_ms * 1e-3) / 1e12, "peak": mfma_peak,
+                "unit": "TOP/s" if dominant == "fwd_v7" else "TFLOP/s"}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = traffic
     result = {
         "metric": "quantized-MAC/s + fwd+bwd ms per ResNet-20 w3a3 CiM layer, batch 256",
         "value": value,
@@ -260,11 +289,11 @@ def main():
                    "per_gpu_batch": args.batch, "xbar": XBAR, "adc_bits": ADC, "first_layer": "w8a8",
                    "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3),
                    "launch": "hip_graph" if graph else "eager"},
-        "roofline": {"bound": "hbm", "kernel": _lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]],
-                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                     "traffic": None, "avg_launch_us": avg_launch_ms * 1e3, "launches": kt.launches,
-                     "algo_bytes_per_launch": kt.algo_bytes / max(kt.launches, 1),
-                     "algo_tflops": kt.algo_flops / max(kt.launches, 1) / (avg_launch_ms * 1e-3) / 1e12},
+        "roofline": dict(roof, kernel=_lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]],
+                         avg_launch_us=avg_launch_ms * 1e3, launches=kt.launches,
+                         algo_bytes_per_launch=bytes_l, algo_flops_per_launch=flops_l,
+                         t_hbm_us=t_hbm * 1e6, t_mfma_us=t_mfma * 1e6,
+                         traffic_source=os.path.relpath(TRAFFIC_JSON, REPO) if traffic is not None else None),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
     }

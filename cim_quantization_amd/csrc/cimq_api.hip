@@ -378,7 +378,13 @@ int set_lds(K kernel, size_t bytes) {
 // one kernel id, recorded on the launch stream; algorithmic bytes / flops per launch follow
 // SURVEY.md section 8(d) (fp32 tensors the kernel must read or write once).
 // ---------------------------------------------------------------------------------------
-enum KernelId { KID_NONE = 0, KID_FWD = 1, KID_BWD_GX = 2, KID_BWD_GW = 3, KID_PREP_ACT = 4 };
+// 1-4: every launch of that role (all kernel variants); 5-7: only the v7-path kernels
+// (cim_fwd_v3_kernel<4, KS, true>, cim_bwd_gx_v8_kernel, cim_bwd_gw_v7_kernel), so that one
+// id maps to the launches of one rocprof kernel symbol family
+enum KernelId {
+  KID_NONE = 0, KID_FWD = 1, KID_BWD_GX = 2, KID_BWD_GW = 3, KID_PREP_ACT = 4,
+  KID_FWD_V7 = 5, KID_GX_V8 = 6, KID_GW_V7 = 7, KID_LAST = 7
+};
 
 struct Profiler {
   std::mutex mu;
@@ -396,8 +402,11 @@ void algo_counts(const Geo& g, int kid, double* bytes, double* flops) {
   const double x4 = 4.0 * (double)g.Nin, y4 = 4.0 * (double)g.M * g.O;
   const double mac = (double)g.M * g.O * g.K;
   switch (kid) {
+    case KID_FWD_V7:
     case KID_FWD: *bytes = x4 + y4; *flops = 2.0 * mac; break;             // read x, write y
+    case KID_GX_V8:
     case KID_BWD_GX: *bytes = 2.0 * x4 + y4; *flops = 2.0 * mac * g.nbw; break;  // read gy, x; write gx
+    case KID_GW_V7:
     case KID_BWD_GW: *bytes = x4 + y4; *flops = 2.0 * mac * g.nba; break;  // read gy, x
     case KID_PREP_ACT: *bytes = x4 + (double)g.Nin * (g.NBP + 1); *flops = 0; break;
     default: *bytes = 0; *flops = 0;
@@ -408,7 +417,9 @@ void algo_counts(const Geo& g, int kid, double* bytes, double* flops) {
 int prof_begin(int kid, const Geo& g, hipStream_t s) {
   Profiler& p = prof();
   std::lock_guard<std::mutex> lk(p.mu);
-  if (p.kid != kid || p.n >= p.cap) return -1;
+  if (p.n >= p.cap) return -1;
+  const int role = kid == KID_FWD_V7 ? KID_FWD : kid == KID_GX_V8 ? KID_BWD_GX : kid == KID_GW_V7 ? KID_BWD_GW : kid;
+  if (p.kid != kid && p.kid != role) return -1;
   const int slot = p.n++;
   double b, f;
   algo_counts(g, kid, &b, &f);
@@ -477,10 +488,11 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
                   hipStream_t s) {
   CtxLayout L = ctx_layout(g);
   // compact state words when the v7 backward will read them
-  auto kern = v7_plan(g).ok ? cim_fwd_v3_kernel<NBP, KS, true> : cim_fwd_v3_kernel<NBP, KS, false>;
+  const bool cst = v7_plan(g).ok;
+  auto kern = cst ? cim_fwd_v3_kernel<NBP, KS, true> : cim_fwd_v3_kernel<NBP, KS, false>;
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
   dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, 4));
-  const int slot = prof_begin(KID_FWD, g, s);
+  const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
                      reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);
   prof_end(slot, s);
@@ -622,7 +634,7 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   {
     auto kern = lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false>;
     CIMQ_TRY(set_lds(kern, p.lds_gx));
-    const int slot = prof_begin(KID_BWD_GX, g, s);
+    const int slot = prof_begin(KID_GX_V8, g, s);
     hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256), p.lds_gx, s, g, p.v, st,
                        reinterpret_cast<const v4i*>(ctx + L.wcy), pp, sw, sa, gout, x, gx,
                        reinterpret_cast<float*>(ws + W.lsq_part));
@@ -632,7 +644,7 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   {
     auto kern = cim_bwd_gw_v7_kernel<NBW, NBA>;
     CIMQ_TRY(set_lds(kern, p.lds_gw));
-    const int slot = prof_begin(KID_BWD_GW, g, s);
+    const int slot = prof_begin(KID_GW_V7, g, s);
     hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(256), p.lds_gw, s, g, p.v, st, ctx + L.xhat, pp,
                        gout, reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
     prof_end(slot, s);
@@ -981,7 +993,7 @@ int cimq_profile_start(int kernel_id, int max_launches) {
   Profiler& p = prof();
   std::lock_guard<std::mutex> lk(p.mu);
   if (p.ev) return fail(CIMQ_EINVAL, "profiler already running");
-  if (kernel_id < KID_FWD || kernel_id > KID_PREP_ACT || max_launches <= 0)
+  if (kernel_id < KID_FWD || kernel_id > KID_LAST || max_launches <= 0)
     return fail(CIMQ_EINVAL, "bad profiler arguments");
   p.ev = new hipEvent_t[2 * (size_t)max_launches];
   for (int i = 0; i < 2 * max_launches; ++i) {

@@ -438,7 +438,11 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) {
           const int o = (og * 4 + ob) * 16 + r16;
+#ifdef CIMQ_EXP_FWD_NOST
+          if (stc[ob][0] == 0x7fffffffu) {
+#else
           if (ob < nob && o < g.O) {
+#endif
             uint32_t* s32 = reinterpret_cast<uint32_t*>(st) + ((size_t)i * g.M + (size_t)mt * 64 + wave * 16 + 4 * g4) * g.O + o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stc[ob][r];
@@ -1102,7 +1106,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
 // state words are read straight from memory, one pixel tile ahead.
 // ---------------------------------------------------------------------------------------
 template <int NBP, int FBX, int NBWX>
-__global__ __launch_bounds__(256, 3) void cim_bwd_gw_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
+__global__ __launch_bounds__(256, 1) void cim_bwd_gw_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
                                                                const uint8_t* __restrict__ xcb, Params pp,
                                                                const float* __restrict__ gout, int rows_per_chunk,
                                                                float* __restrict__ gw_slab, float* __restrict__ ga_slab) {

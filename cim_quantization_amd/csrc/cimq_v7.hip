@@ -179,6 +179,10 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
           v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < NKS; ++s) {
+#ifdef CIMQ_EXP_GX_NOMFMA
+            acc[0] += (float)Gh[s][0] + (float)Gm[s][1] + (float)Gl[s][2];
+            continue;
+#endif
             const v8bf a = as_v8bf(wt[(cb * NKS + s) * 64]);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gh[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gm[s], acc, 0, 0, 0);
@@ -191,7 +195,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
           if (col == 0) fp = 0.f;
           const float y = (acc[1] + fn) + fp;
           const int cp = (cpb_lo + cb) * 4 + g4;
+#ifdef CIMQ_EXP_GX_NORING
+          if (y == 1234.5f) {
+#else
           if (pv && cp < CPP) {
+#endif
             float* e = rr + cp * RE;
             if (cb == 0 && shared_first) {
               e[col + 1] += y;
@@ -471,11 +479,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   v4f acc[9];
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp) acc[tp] = v4f{0.f, 0.f, 0.f, 0.f};
-  float qs[3][NKJ];
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int c = 0; c < NKJ; ++c) qs[a][c] = 0.f;
+  // grad_alpha partials accumulate in LDS, one region per wave: red[wave][tl][kj][16 o]
+  for (int t = threadIdx.x; t < 4 * 3 * NKJ * 16; t += blockDim.x) red[t] = 0.f;
 
   // Software pipeline over the chunk's stages: the global loads of stage n+1 (source words of
   // the staged rows, state words and grad_out of this lane's K-step) are issued before the
@@ -484,8 +489,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   const int nit = 16 * v.NSLOT * ng8;  // staging items (<= 2 per thread, v7_plan)
   struct Pref {
     uint32_t w[2][10];
-    uint32_t sv[3][8];
-    float gv[8];
   };
   auto stage_geom = [&](int stg, int& b0, int& ih_first) {
     const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
@@ -517,31 +520,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         }
       }
     }
-    const size_t mk8 = ((size_t)chunk * v.nstage + stg) * 128 + 32 * wave + 8 * g4;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pf.gv[e] = 0.f;
-#pragma unroll
-    for (int tl = 0; tl < 3; ++tl)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pf.sv[tl][e] = 0u;
-    if (mk8 < (size_t)g.M) {
-      const int b = (int)(mk8 / g.P);
-      const int pimg = (int)(mk8 - (size_t)b * g.P);
-      if (g.onchw) {
-        const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
-        const float4 a0 = gp[0], a1 = gp[1];
-        pf.gv[0] = a0.x; pf.gv[1] = a0.y; pf.gv[2] = a0.z; pf.gv[3] = a0.w;
-        pf.gv[4] = a1.x; pf.gv[5] = a1.y; pf.gv[6] = a1.z; pf.gv[7] = a1.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) pf.gv[e] = gout[(mk8 + e) * g.O + o];
-      }
-#pragma unroll
-      for (int tl = 0; tl < 3; ++tl)
-        if (tl < ntl)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) pf.sv[tl][e] = st[((size_t)(i_lo + tl) * g.M + mk8 + e) * g.O + o];
-    }
   };
 
   Pref pf;
@@ -554,7 +532,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
     for (int u2 = 0; u2 < 2; ++u2) {
       const int it = threadIdx.x + u2 * 256;
+#ifdef CIMQ_EXP_GW_NOSTAGE
+      if (it < 0) {
+#else
       if (it < nit) {
+#endif
         const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
         const int slot = rem / ng8, c8 = rem - slot * ng8;
 #pragma unroll
@@ -575,14 +557,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         }
       }
     }
-    float gv[8];
-    uint32_t svc[3][8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) gv[e] = pf.gv[e];
-#pragma unroll
-    for (int tl = 0; tl < 3; ++tl)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) svc[tl][e] = pf.sv[tl][e];
     __syncthreads();
     if (stg + 1 < v.nstage) load(stg + 1, pf);
     // this wave's K-step: pixels mk .. mk+31; this lane's 8 pixels mk8 .. mk8+7 (one row)
@@ -591,6 +565,16 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     const int b = (int)(mk8 / g.P);
     const int pimg = (int)(mk8 - (size_t)b * g.P);
     const int oh = pimg >> v.lw, ow0 = pimg & (Wo - 1);
+    float gv[8];
+    if (g.onchw) {
+      const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
+      const float4 a0 = gp[0], a1 = gp[1];
+      gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
+      gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = gout[(mk8 + e) * g.O + o];
+    }
     // row slot of each kernel row for this lane's output row (-1: outside the image)
     int slot_kh[3];
 #pragma unroll
@@ -600,23 +584,32 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
       if (ih >= 0 && ih < g.H) sl = v.whole ? (b - b0) * g.H + ih : ih - ih_first;
       slot_kh[kh] = sl;
     }
-#pragma unroll
+#pragma unroll 1
     for (int tl = 0; tl < 3; ++tl) {
       if (tl < ntl) {
         const int i = i_lo + tl;
-        const uint32_t* sv = svc[tl];
+        uint32_t sv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
         // grad_alpha partials (lsq.py:321-333): sum over the pixels of code * g
+#ifdef CIMQ_EXP_GW_NOGA
+        if (false) {
+#else
         if (((i * g.xbar) / KHW) / 16 == cb) {
+#endif
 #pragma unroll
           for (int kj = 0; kj < NKJ; ++kj) {
             float q = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const uint32_t bits = sv[e] >> (3 * kj);
-              const float t = (bits & 4u) ? -gv[e] : gv[e];
-              q += (bits & 2u) ? t : 0.f;
+              // code * g as bit ops: sign <- bit 3kj+2 (code < 0), mask <- bit 3kj+1 (code != 0)
+              const uint32_t nzm = (uint32_t)(((int)(sv[e] << (30 - 3 * kj))) >> 31);
+              const uint32_t sgn = (sv[e] << (29 - 3 * kj)) & 0x80000000u;
+              q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
             }
-            qs[tl][kj] += q;
+            q += __shfl_xor(q, 16);
+            q += __shfl_xor(q, 32);
+            if (g4 == 0) red[((wave * 3 + tl) * NKJ + kj) * 16 + r16] += q;
           }
         }
         // B operands: g * D_j, D_j = sum_k cD_kj * pass_ijk, split into bf16 hi / mid / lo
@@ -638,23 +631,34 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           }
           split3x8(d, bh[j], bm[j], bq[j]);
         }
-#pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
+        // A fragments of a tap (rows of other tiles and kernel rows outside the image are
+        // zeroed by a select, no branch)
+        auto read_tap = [&](int tp, v4i (&dst)[NBA]) {
           const int kh = tp / 3, kw = tp - 3 * (tp / 3);
           const int sl = slot_kh[kh];
           const bool ok = (tit[tp] == i) && sl >= 0;
-          if (__any(ok)) {
+          const __bf16* src = pl + ((size_t)kw * 16 + r16) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
 #pragma unroll
-            for (int j = 0; j < NBA; ++j) {
-              v4i av = {0, 0, 0, 0};
-              if (ok)
-                av = *reinterpret_cast<const v4i*>(pl + ((size_t)(j * 3 + kw) * 16 + r16) * v.CPITCH + sl * Wo + ow0);
-              const v8bf a = as_v8bf(av);
-              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
-              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
-              acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
-            }
+          for (int j = 0; j < NBA; ++j) {
+            const v4i a = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * 16 * v.CPITCH);
+            dst[j] = ok ? a : v4i{0, 0, 0, 0};
           }
+        };
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          v4i acur[NBA];
+          read_tap(tp, acur);
+#ifndef CIMQ_EXP_GW_NOMFMA
+#pragma unroll
+          for (int j = 0; j < NBA; ++j) {
+            const v8bf a = as_v8bf(acur[j]);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
+          }
+#else
+          acc[tp][0] += (float)acur[0][0];
+#endif
         }
       }
     }
@@ -667,16 +671,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gred[((wave * 9 + tp) * 16 + 4 * g4 + r) * 16 + r16] = acc[tp][r];
-#pragma unroll
-  for (int tl = 0; tl < 3; ++tl)
-    if (tl < ntl)
-#pragma unroll
-      for (int kj = 0; kj < NKJ; ++kj) {
-        float q = qs[tl][kj];
-        q += __shfl_xor(q, 16);
-        q += __shfl_xor(q, 32);
-        if (g4 == 0) red[((wave * 3 + tl) * NKJ + kj) * 16 + r16] = q;
-      }
   __syncthreads();
   const int FR = g.FBT * 16;
   for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) {

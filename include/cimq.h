@@ -156,7 +156,8 @@ int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float
                             void* ctx, void* stream);
 
 /* Diagnostic kernel timer.  Until cimq_profile_stop(), every launch of kernel ``kernel_id``
- * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep) is
+ * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep, each over
+ * all kernel variants; 5 / 6 / 7 = only the v7-path forward / grad_x / grad_w kernels) is
  * bracketed by a hipEvent pair on its launch stream (at most ``max_launches``).  stop()
  * waits for the last event and returns the summed kernel time, the number of launches and
  * their summed algorithmic bytes / flops ("Roofline accounting"). */

@@ -20,13 +20,15 @@ sys.path.insert(0, REPO)
 # name -> preprocessor defines; kernels carry CIMQ_EXP_* knobs only while an experiment runs
 VARIANTS = {
     "base": [],
-    "gx_v5": ["CIMQ_GX_V5"],
-    "noA": ["CIMQ_EXP_NO_PHASEA"],
-    "noB": ["CIMQ_EXP_NO_PHASEB"],
-    "noW": ["CIMQ_EXP_NO_WSTAGE"],
-    "noDMA": ["CIMQ_EXP_NO_DMA"],
-    "noAB": ["CIMQ_EXP_NO_PHASEA", "CIMQ_EXP_NO_PHASEB"],
+    "gw_noga": ["CIMQ_EXP_GW_NOGA"],
+    "gw_nomfma": ["CIMQ_EXP_GW_NOMFMA"],
+    "gw_nostage": ["CIMQ_EXP_GW_NOSTAGE"],
+    "gx_nomfma": ["CIMQ_EXP_GX_NOMFMA"],
+    "gx_noring": ["CIMQ_EXP_GX_NORING"],
+    "fwd_nost": ["CIMQ_EXP_FWD_NOST"],
 }
+if os.environ.get("CIMQ_EXP_VARIANTS"):
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
 
 
 def lib_path(name):
@@ -59,7 +61,7 @@ def do_time(layer, iters):
         m(x1).backward(g)  # warm (alpha init etc.)
         torch.cuda.synchronize()
         res = {}
-        for kern in ("fwd", "bwd_gx", "bwd_gw"):
+        for kern in ("fwd", "bwd_gx", "bwd_gw", "prep_act"):
             with _lib.KernelTimer(kern) as kt:
                 for _ in range(iters):
                     x1 = x.detach().requires_grad_(True)
