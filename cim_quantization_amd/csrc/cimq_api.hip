@@ -489,7 +489,10 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   CtxLayout L = ctx_layout(g);
   // compact state words when the v7 backward will read them
   const bool cst = v7_plan(g).ok;
-  auto kern = cst ? cim_fwd_v3_kernel<NBP, KS, true> : cim_fwd_v3_kernel<NBP, KS, false>;
+  // OBM: 16-channel output blocks per block (register arrays sized for exactly that)
+  auto kern = g.OB16 == 1 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 1> : cim_fwd_v3_kernel<NBP, KS, false, 1>)
+            : g.OB16 == 2 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 2> : cim_fwd_v3_kernel<NBP, KS, false, 2>)
+                          : (cst ? cim_fwd_v3_kernel<NBP, KS, true, 4> : cim_fwd_v3_kernel<NBP, KS, false, 4>);
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
   dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, 4));
   const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);

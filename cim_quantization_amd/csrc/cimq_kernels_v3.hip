@@ -278,7 +278,7 @@ __device__ inline uint32_t st_bits(bool pass, float code) {
 
 // CST: compact state words (cimq_v7.hip) -- one uint32 per (tile i, pixel m, channel o) at
 // st32[(i*M + m)*O + o], bits 3*(k*nba + j) + {0: STE pass, 1: code != 0, 2: code < 0}.
-template <int NBP, int KS, bool CST>
+template <int NBP, int KS, bool CST, int OBM>
 __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
@@ -287,8 +287,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   typedef typename StWord<NBP>::T SW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int og = blockIdx.y;
-  const int NOB = min(4, g.OB16);
-  const int nob = min(4, g.OB16 - og * 4);
+  const int NOB = min(OBM, g.OB16);
+  const int nob = min(OBM, g.OB16 - og * OBM);
   const int TT = v.fwd_res ? g.T : 1;
   const int nkj = g.nbw * g.nba;
   uint8_t* cur = smem;
@@ -313,13 +313,13 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const int l = idx & 63, fr = idx >> 6;
       const int ks = fr % KS, kob = fr / KS, k = kob / NOB, ob = kob - k * NOB;
       v4i w = {0, 0, 0, 0};
-      if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * 4 + ob) * WAVE + l];
+      if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
       return w;
     });
     if (!flag_lit) {
       batched_copy<2>(nkj * NOB * 16, prm + (size_t)tt * nkj * NOB * 16, [&](int idx) -> int4 {
         const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
-        const int o = og * 64 + col;
+        const int o = og * OBM * 16 + col;
         int4 p = make_int4(0, 0, 0, 0);
         if (o < g.Opad) {
           const int pi = pidx(g, i, j, k, o);
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       });
       batched_copy<4>(nkj * NOB * 16, cfl + (size_t)tt * nkj * NOB * 16, [&](int idx) -> float {
         const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
-        const int o = og * 64 + col;
+        const int o = og * OBM * 16 + col;
         return (o < g.Opad) ? pp.coef[pidx(g, i, j, k, o)] : 0.f;
       });
     }
@@ -351,9 +351,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     __syncthreads();
     stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
     __syncthreads();
-    float acc[4][4];
+    float acc[OBM][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < OBM; ++a)
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[a][c] = 0.f;
     for (int i = 0; i < g.T; ++i) {
@@ -369,16 +369,16 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
       const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
-      uint32_t stc[4][4];
+      uint32_t stc[OBM][4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < OBM; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) stc[a][c] = 0u;
       for (int k = 0; k < g.nbw; ++k) {
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
+        for (int ob = 0; ob < OBM; ++ob) {
           if (ob < nob) {
-            const int o = (og * 4 + ob) * 16 + r16;
+            const int o = (og * OBM + ob) * 16 + r16;
             v4i wk[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) wk[ks] = wt[((k * NOB + ob) * KS + ks) * 64 + lane];
@@ -436,8 +436,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       }
       if (CST) {
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-          const int o = (og * 4 + ob) * 16 + r16;
+        for (int ob = 0; ob < OBM; ++ob) {
+          const int o = (og * OBM + ob) * 16 + r16;
 #ifdef CIMQ_EXP_FWD_NOST
           if (stc[ob][0] == 0x7fffffffu) {
 #else
@@ -452,8 +452,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     }
     // acc[ob][r]: pixel wave*16 + 4*g4 + r, channel (og*4 + ob)*16 + r16
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int o = (og * 4 + ob) * 16 + r16;
+    for (int ob = 0; ob < OBM; ++ob) {
+      const int o = (og * OBM + ob) * 16 + r16;
       if (ob < nob && o < g.O) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
