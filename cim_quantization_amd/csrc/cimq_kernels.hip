@@ -72,14 +72,91 @@ __device__ inline void act_item(const Geo& g, const float* __restrict__ x, float
   pack_word(bw, g.NBP, xcb, idx);
 }
 
+// Slice words of one element, NBP-specialised.  When x_int is an exact integer (the common
+// case: fl(fl(r*sa)/sa) == r) the floor / remainder chain of slicing_act(_signed) reduces to
+// shifts and masks of that integer, bit for bit (floor-mod by 2^b of an integer is its low b
+// bits in two's complement); other values (the 6 - eps slice artifacts) take the float path.
+template <int NBP>
+__device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint32_t (&fwd)[NBP / 4],
+                                 uint32_t (&bwd)[NBP / 4]) {
+  float xq;
+  if (g.input_kind == 1) {
+    const float t = v / sa;
+    const float c = clamp_nan(t, 0.f, g.lsq_qp);
+    const float r = rintf(c);
+    const float rp = (r - c) + c;  // round_pass value
+    xq = rp * sa;
+  } else {
+    xq = v;
+  }
+  const float xi = xq / sa;
+  const int xhi = to_i8_wrap(xi);
+  const int mask = (1 << g.bsa) - 1;
+  const bool xi_int = (xi == rintf(xi)) && fabsf(xi) < 16777216.f;
+  const int xii = xi_int ? (int)xi : 0;
+#pragma unroll
+  for (int w = 0; w < NBP / 4; ++w) { fwd[w] = 0u; bwd[w] = 0u; }
+#pragma unroll
+  for (int j = 0; j < NBP; ++j) {
+    if (j < g.nba) {
+      int sf, sb;
+      const int sh = g.bsa * j;
+      if (sgn) {
+        sb = xhi >= 0 ? ((xhi >> sh) & mask) : -(((-xhi) >> sh) & mask);
+        sf = xii >= 0 ? ((xii >> sh) & mask) : -(((-xii) >> sh) & mask);
+      } else {
+        sb = (xhi >> sh) & mask;
+        sf = (xii >> sh) & mask;
+      }
+      if (!xi_int) sf = clamp_i8(sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa));
+      fwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sf << (8 * (j & 3));
+      bwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sb << (8 * (j & 3));
+    }
+  }
+}
+
+// four consecutive elements (idx4 = 4 * t): one 16-B load, 16-B (NBP 4) or 2 x 16-B stores
+template <int NBP>
+__device__ inline void act_item4(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
+                                 uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long t) {
+  const float4 v4 = reinterpret_cast<const float4*>(x)[t];
+  const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+  uint32_t f[4][NBP / 4], b[4][NBP / 4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) act_words<NBP>(g, vv[e], sa, sgn, f[e], b[e]);
+  if (NBP == 4) {
+    reinterpret_cast<uint4*>(xcf)[t] = make_uint4(f[0][0], f[1][0], f[2][0], f[3][0]);
+    reinterpret_cast<uint4*>(xcb)[t] = make_uint4(b[0][0], b[1][0], b[2][0], b[3][0]);
+  } else {
+    reinterpret_cast<uint4*>(xcf)[2 * t] = make_uint4(f[0][0], f[0][NBP / 4 - 1], f[1][0], f[1][NBP / 4 - 1]);
+    reinterpret_cast<uint4*>(xcf)[2 * t + 1] = make_uint4(f[2][0], f[2][NBP / 4 - 1], f[3][0], f[3][NBP / 4 - 1]);
+    reinterpret_cast<uint4*>(xcb)[2 * t] = make_uint4(b[0][0], b[0][NBP / 4 - 1], b[1][0], b[1][NBP / 4 - 1]);
+    reinterpret_cast<uint4*>(xcb)[2 * t + 1] = make_uint4(b[2][0], b[2][NBP / 4 - 1], b[3][0], b[3][NBP / 4 - 1]);
+  }
+}
+
+// all elements of x: vectorised when Nin % 4 == 0 (W % 4 == 0), element-wise otherwise
+__device__ inline void act_range(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
+                                 uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long first,
+                                 long long step) {
+  if (g.Nin % 4 == 0) {
+    const long long n4 = g.Nin / 4;
+    if (g.NBP == 4)
+      for (long long t = first; t < n4; t += step) act_item4<4>(g, x, sa, sgn, xcf, xcb, t);
+    else
+      for (long long t = first; t < n4; t += step) act_item4<8>(g, x, sa, sgn, xcf, xcb, t);
+  } else {
+    for (long long idx = first; idx < g.Nin; idx += step) act_item(g, x, sa, sgn, xcf, xcb, idx);
+  }
+}
+
 __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ sa_p,
                                 const float* __restrict__ signed_p, uint8_t* __restrict__ xcf,
                                 uint8_t* __restrict__ xcb) {
   const float sa = *sa_p;
   const bool sgn = (*signed_p) != 0.f;
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < g.Nin;
-       idx += (long long)gridDim.x * blockDim.x)
-    act_item(g, x, sa, sgn, xcf, xcb, idx);
+  act_range(g, x, sa, sgn, xcf, xcb, (long long)blockIdx.x * blockDim.x + threadIdx.x,
+            (long long)gridDim.x * blockDim.x);
 }
 
 // =========================================================================================

@@ -105,9 +105,8 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
   if ((int)blockIdx.x >= nwblk) {
     const int ab = (int)blockIdx.x - nwblk;
     const bool sgn = a.signed_act[0] != 0.f;
-    const long long step = (long long)a.nact_blocks * blockDim.x;
-    for (long long idx = (long long)ab * blockDim.x + threadIdx.x; idx < g.Nin; idx += step)
-      act_item(g, a.x, sa, sgn, a.xcf, a.xcb, idx);
+    act_range(g, a.x, sa, sgn, a.xcf, a.xcb, (long long)ab * blockDim.x + threadIdx.x,
+              (long long)a.nact_blocks * blockDim.x);
     return;
   }
   const float sw = grad_scale_value(a.alpha_w[0], q.gs_w);  // lsq.py:553-554
