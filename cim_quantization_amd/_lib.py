@@ -12,7 +12,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcimq.so")
+LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
 ABI_VERSION = 3
 
 CIMQ_INPUT_XQ = 0

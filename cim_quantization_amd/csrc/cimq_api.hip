@@ -199,6 +199,7 @@ inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
 Plan3 v3_plan(const Geo& g) {
   Plan3 p;
   memset(&p, 0, sizeof(p));
+  if (tune("V3", 1) == 0) return p;  // experiments: force the general kernels
   if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0 || g.Wo < 4) return p;
   if (g.O > 256 || 256 % g.O != 0) return p;  // grad_alpha reducer: one thread per channel
   if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
@@ -286,7 +287,7 @@ Plan7 v7_plan(const Geo& g) {
   if (!((g.nbw == 3 && g.nba == 3) || (g.nbw == 2 && g.nba == 2))) return p;  // instantiated slice pairs
   if (g.O % 16 != 0 || !(g.OB16 == 1 || g.OB16 == 2 || g.OB16 == 4)) return p;
   // 3x3, stride 1, pad 1 ("same" conv: every CiM conv of the CIFAR ResNets but the downsampling ones)
-  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1) return p;
+  if (g.KH != 3 || g.KW != 3 || g.SH != g.SW || g.SH > 2 || g.PH != 1 || g.PW != 1) return p;
   if (g.Wo % 8 != 0 || (g.Wo & (g.Wo - 1)) != 0 || g.Wo > 64 || g.M % 128 != 0 || g.FBT > 8) return p;
   V7& v = p.v;
   if (g.P % 128 == 0) v.whole = 0;
@@ -308,13 +309,13 @@ Plan7 v7_plan(const Geo& g) {
   v.NRS = 64 / g.Wo;
   if (v.NRS < 1) return p;
   v.RSLOT = v.NRS + 2;
-  p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (v.SWD + 2) * 4) + 64 * 4 + 64;
+  p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (g.SH * v.SWD + 2) * 4) + 64 * 4 + 64;
   // grad_w
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
   v.CPITCH = v.NSLOT * g.Wo + 8;
   const size_t planes = (size_t)g.nba * g.KW * 16 * v.CPITCH * 2;
   p.lds_gw = std::max(a16(planes), (size_t)4 * 9 * 256 * 4) + 64 * 4 + (size_t)4 * 3 * g.nbw * g.nba * 16 * 4;
-  if (16 * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
+  if (g.SH == 1 && 16 * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
   p.pairs = ((g.C + 15) / 16) * g.OB16;
   const int stages = g.M / 128;
   const int want = std::max(1, tune("GW_BLOCKS", 512) / p.pairs);
@@ -635,7 +636,8 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
   {
-    auto kern = lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false>;
+    auto kern = g.SH == 1 ? (lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true, 1> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false, 1>)
+                          : (lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true, 2> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false, 2>);
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_GX_V8, g, s);
     hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256), p.lds_gx, s, g, p.v, st,
@@ -645,7 +647,7 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
     CIMQ_TRY(check_hip("cim_bwd_gx_v8"));
   }
   {
-    auto kern = cim_bwd_gw_v7_kernel<NBW, NBA>;
+    auto kern = g.SH == 1 ? cim_bwd_gw_v7_kernel<NBW, NBA, 1> : cim_bwd_gw_v7_kernel<NBW, NBA, 2>;
     CIMQ_TRY(set_lds(kern, p.lds_gw));
     const int slot = prof_begin(KID_GW_V7, g, s);
     hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(256), p.lds_gw, s, g, p.v, st, ctx + L.xhat, pp,

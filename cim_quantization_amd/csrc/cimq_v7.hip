@@ -81,7 +81,7 @@ __device__ inline float dpp_from_prev(float v) {
 // contributing output rows are done are folded along kh, scaled, run through the LSQ act
 // backward and stored -- no atomics, every value written by exactly one lane.
 // ---------------------------------------------------------------------------------------
-template <int NBW, int NBA, int OBX, bool LSQ>
+template <int NBW, int NBA, int OBX, bool LSQ, int SS>
 __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
                                                             const v4i* __restrict__ wcy, Params pp,
                                                             const float* __restrict__ sw_p,
@@ -94,10 +94,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
   const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB);
-  const int oh_lo = max(0, r0 - 1), oh_hi = min(g.Ho - 1, r1);
+  // output rows whose windows touch input rows [r0, r1) (pad 1, 3 kernel rows, stride SS)
+  const int oh_lo = max(0, (r0 + 1 - 2 + SS - 1) / SS), oh_hi = min(g.Ho - 1, (r1 - 1 + 1) / SS);
   const int nsteps = (oh_hi - oh_lo + v.NRS) / v.NRS;
   const int CPP = g.C * 3;
-  const int RE = v.SWD + 2;
+  const int RE = SS * v.SWD + 2;  // ring entry: input columns -1 .. SS*SWD (local), + pad
   const int rrow = v.NSEG * CPP * RE;  // floats per ring row
   float* ring = reinterpret_cast<float*>(smem);
   float* cel = ring + (size_t)v.RSLOT * rrow;
@@ -188,27 +189,46 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gm[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gl[s], acc, 0, 0, 0);
           }
-          // acc[kw] = gx_unf[(cp, kw)][this lane's pixel], cp = (cpb_lo + cb)*4 + g4
-          float fn = dpp_from_next(acc[0]);  // kw = 0 of pixel ow + 1 -> iw = ow
-          float fp = dpp_from_prev(acc[2]);  // kw = 2 of pixel ow - 1 -> iw = ow
+          // acc[kw] = gx_unf[(cp, kw)][this lane's pixel], cp = (cpb_lo + cb)*4 + g4; pixel ow
+          // feeds input column SS*ow + kw - 1
+          float fn = dpp_from_next(acc[0]);  // kw = 0 of pixel ow + 1
           if (col == v.SWD - 1) fn = 0.f;
-          if (col == 0) fp = 0.f;
-          const float y = (acc[1] + fn) + fp;
           const int cp = (cpb_lo + cb) * 4 + g4;
+          const bool acc_mode = cb == 0 && shared_first;
+          if (SS == 1) {
+            float fp = dpp_from_prev(acc[2]);  // kw = 2 of pixel ow - 1 -> iw = ow
+            if (col == 0) fp = 0.f;
+            const float y = (acc[1] + fn) + fp;
 #ifdef CIMQ_EXP_GX_NORING
-          if (y == 1234.5f) {
+            if (y == 1234.5f) {
 #else
-          if (pv && cp < CPP) {
+            if (pv && cp < CPP) {
 #endif
-            float* e = rr + cp * RE;
-            if (cb == 0 && shared_first) {
-              e[col + 1] += y;
-              if (col == 0) e[0] += acc[0];
-              if (col == v.SWD - 1) e[v.SWD + 1] += acc[2];
-            } else {
-              e[col + 1] = y;
-              if (col == 0) e[0] = acc[0];
-              if (col == v.SWD - 1) e[v.SWD + 1] = acc[2];
+              float* e = rr + cp * RE;
+              if (acc_mode) {
+                e[col + 1] += y;
+                if (col == 0) e[0] += acc[0];
+                if (col == v.SWD - 1) e[v.SWD + 1] += acc[2];
+              } else {
+                e[col + 1] = y;
+                if (col == 0) e[0] = acc[0];
+                if (col == v.SWD - 1) e[v.SWD + 1] = acc[2];
+              }
+            }
+          } else {
+            // stride 2: even column 2ow <- kw 1; odd column 2ow + 1 <- kw 2 of ow, kw 0 of ow + 1
+            const float ye = acc[1], yo = acc[2] + fn;
+            if (pv && cp < CPP) {
+              float* e = rr + cp * RE;
+              if (acc_mode) {
+                e[2 * col + 1] += ye;
+                e[2 * col + 2] += yo;
+                if (col == 0) e[0] += acc[0];
+              } else {
+                e[2 * col + 1] = ye;
+                e[2 * col + 2] = yo;
+                if (col == 0) e[0] = acc[0];
+              }
             }
           }
         }
@@ -216,23 +236,25 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
     }
     __syncthreads();
     // fold along kh the input rows whose contributing output rows are all in the ring
-    const int upto = (oh_e == g.Ho - 1) ? g.H - 1 : oh_e - 1;
+    // input row ih is complete once floor((ih + 1) / SS) <= oh_e
+    const int upto = (oh_e == g.Ho - 1) ? g.H - 1 : (oh_e + 1) * SS - 2;
     const int f0 = max(done + 1, r0), f1 = min(upto, r1 - 1);
     if (f1 >= f0) {
       const int nf = (f1 - f0 + 1) * g.C * g.W;
       for (int t = threadIdx.x; t < nf; t += blockDim.x) {
         const int iw = t % g.W, rest = t / g.W;
         const int c = rest % g.C, ih = f0 + rest / g.C;
-        const int sg = iw / v.SWD, cl = iw - sg * v.SWD;
+        const int sg = iw / (SS * v.SWD), cl = iw - sg * (SS * v.SWD);
         float a = 0.f;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          const int oo = ih + 1 - kh;
-          if (oo >= oh_lo && oo <= oh_e) {
+          const int oo2 = ih + 1 - kh;  // = SS * oh
+          const int oo = oo2 / SS;
+          if (oo2 >= 0 && oo * SS == oo2 && oo >= oh_lo && oo <= oh_e) {
             const float* e = ring + (size_t)((oo - oh_lo) % v.RSLOT) * rrow + (c * 3 + kh) * RE;
             a += e[sg * CPP * RE + cl + 1];
-            if (cl == v.SWD - 1 && sg + 1 < v.NSEG) a += e[(sg + 1) * CPP * RE];
-            if (cl == 0 && sg > 0) a += e[(sg - 1) * CPP * RE + v.SWD + 1];
+            if (cl == SS * v.SWD - 1 && sg + 1 < v.NSEG) a += e[(sg + 1) * CPP * RE];
+            if (SS == 1 && cl == 0 && sg > 0) a += e[(sg - 1) * CPP * RE + v.SWD + 1];
           }
         }
         const size_t gi = (((size_t)b * g.C + c) * g.H + ih) * g.W + iw;
@@ -432,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v7_kernel(Geo g, V7 v, cons
 // block = (pixel chunk, (channel block cb, output block ob)); a chunk is nstage stages of 128
 // output pixels; in a stage wave w owns the 32 pixels 32w..32w+31 (one MFMA K-step).
 // stride 1 (v7_plan); at most 3 crossbar tiles touch one 16-channel block.
-template <int NBW, int NBA>
+template <int NBW, int NBA, int SS>
 __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
                                                             const uint8_t* __restrict__ xcb, Params pp,
                                                             const float* __restrict__ gout,
@@ -494,9 +516,10 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
     b0 = (int)(m0 / g.P);
     const int pim0 = (int)(m0 - (size_t)b0 * g.P);
-    ih_first = v.whole ? 0 : (pim0 >> v.lw) - g.PH;
+    ih_first = v.whole ? 0 : (pim0 >> v.lw) * SS - g.PH;
   };
   auto load = [&](int stg, Pref& pf) {
+    if (SS != 1) return;  // stride 2 stages without prefetch (17 source words per item)
     int b0, ih_first;
     stage_geom(stg, b0, ih_first);
 #pragma unroll
@@ -528,9 +551,48 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     int b0, ih_first;
     stage_geom(stg, b0, ih_first);
     __syncthreads();
+    if (SS == 2) {
+      // stride 2: output column ow reads input column 2 ow + kw - 1 -> 17 words per 8 columns
+      for (int it = threadIdx.x; it < nit; it += blockDim.x) {
+        const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
+        const int slot = rem / ng8, c8 = rem - slot * ng8;
+        int b = b0, ih = ih_first + slot;
+        if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
+        const int c = cb * 16 + cl;
+        uint32_t wv[17];
+#pragma unroll
+        for (int u = 0; u < 17; ++u) wv[u] = 0u;
+        if (c < g.C && ih >= 0 && ih < g.H && b < g.B) {
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 16;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 t4 = reinterpret_cast<const uint4*>(src)[q];
+            wv[1 + 4 * q] = t4.x; wv[2 + 4 * q] = t4.y; wv[3 + 4 * q] = t4.z; wv[4 + 4 * q] = t4.w;
+          }
+          if (c8 > 0) wv[0] = src[-1];
+        }
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+          for (int j = 0; j < NBA; ++j) {
+            uint32_t pk[4];
+#pragma unroll
+            for (int e2 = 0; e2 < 4; ++e2) {
+              const uint32_t w0 = wv[4 * e2 + kw], w1 = wv[4 * e2 + 2 + kw];
+              const float f0 = (float)(int8_t)((w0 >> (8 * j)) & 0xFFu);
+              const float f1 = (float)(int8_t)((w1 >> (8 * j)) & 0xFFu);
+              pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+            }
+            __bf16* dst = pl + ((size_t)(j * 3 + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          }
+        }
+      }
+    }
     // bf16 planes of the staged rows: item (channel cl, slot, 8-column group), kw shifts
 #pragma unroll
     for (int u2 = 0; u2 < 2; ++u2) {
+      if (SS != 1) break;
       const int it = threadIdx.x + u2 * 256;
 #ifdef CIMQ_EXP_GW_NOSTAGE
       if (it < 0) {
@@ -579,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     int slot_kh[3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
-      const int ih = oh - g.PH + kh;
+      const int ih = oh * SS - g.PH + kh;
       int sl = -1;
       if (ih >= 0 && ih < g.H) sl = v.whole ? (b - b0) * g.H + ih : ih - ih_first;
       slot_kh[kh] = sl;

@@ -105,6 +105,17 @@ RANDOM_CASES = [
     dict(B=2, C=16, O=16, H=6, k=3, s=1, p=0, wb=4, ab=4, wbs=2, abs=2, xbar=64, adc=1, signed=0),
     dict(B=3, C=64, O=64, H=8, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
     dict(B=64, C=128, O=96, H=1, k=1, s=1, p=0, wb=4, ab=4, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    # v7 backward (compact state words, grad_x v8, grad_w v7): every stage / fold variant
+    dict(B=2, C=64, O=64, H=8, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    dict(B=2, C=32, O=64, H=16, k=3, s=2, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    dict(B=2, C=16, O=32, H=32, k=3, s=2, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    dict(B=2, C=32, O=32, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=2, ab=2, wbs=1, abs=1, xbar=64, adc=1.5, signed=0),
+    dict(B=2, C=32, O=16, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=64, adc=4, signed=0),
+    # sign ADC: sign(ps) at ps = 0 follows the reference's fp32 residues (slice artifacts,
+    # summation order), so this case uses power-of-two scales: x_int, w_int exact
+    dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1, signed=0, sa=0.125,
+         sw=0.0625),
 ]
 
 
@@ -113,8 +124,8 @@ def _random_inputs(cfg, seed):
     B, C, O, H, k = cfg["B"], cfg["C"], cfg["O"], cfg["H"], cfg["k"]
     qp_a = 2 ** cfg["ab"] - 1
     qn_w, qp_w = co.lsq_weight_params(cfg["wb"])
-    sa = np.array([rng.uniform(0.05, 0.4)], np.float32)
-    sw = np.array([rng.uniform(0.01, 0.3)], np.float32)
+    sa = np.array([cfg.get("sa", rng.uniform(0.05, 0.4))], np.float32)
+    sw = np.array([cfg.get("sw", rng.uniform(0.01, 0.3))], np.float32)
     r = rng.integers(0, qp_a + 1, size=(B, C, H, H)).astype(np.float32)
     r[rng.random(r.shape) < 0.35] = 0
     x_q = (r * sa).astype(np.float32)
