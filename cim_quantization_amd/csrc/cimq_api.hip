@@ -309,6 +309,9 @@ Plan7 v7_plan(const Geo& g) {
   v.NRS = 64 / g.Wo;
   if (v.NRS < 1) return p;
   v.RSLOT = v.NRS + 2;
+  // waves per pixel group: more parallelism where an image has few pixel groups
+  v.NPART = tune("GX_NPART", g.Wo >= 32 ? 1 : 2);
+  if (v.NPART != 1 && v.NPART != 2 && v.NPART != 4) return p;
   p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (g.SH * v.SWD + 2) * 4) + 64 * 4 + 64;
   // grad_w
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
@@ -636,11 +639,15 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
   {
-    auto kern = g.SH == 1 ? (lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true, 1> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false, 1>)
-                          : (lsq ? cim_bwd_gx_v8_kernel<NBW, NBA, OBX, true, 2> : cim_bwd_gx_v8_kernel<NBW, NBA, OBX, false, 2>);
+    const int np = p.v.NPART;
+#define CIMQ_GX8(L, S, N) cim_bwd_gx_v8_kernel<NBW, NBA, OBX, L, S, N>
+#define CIMQ_GX8N(L, S) (np == 1 ? CIMQ_GX8(L, S, 1) : np == 2 ? CIMQ_GX8(L, S, 2) : CIMQ_GX8(L, S, 4))
+    auto kern = g.SH == 1 ? (lsq ? CIMQ_GX8N(true, 1) : CIMQ_GX8N(false, 1)) : (lsq ? CIMQ_GX8N(true, 2) : CIMQ_GX8N(false, 2));
+#undef CIMQ_GX8N
+#undef CIMQ_GX8
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_GX_V8, g, s);
-    hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256), p.lds_gx, s, g, p.v, st,
+    hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256 * np), p.lds_gx, s, g, p.v, st,
                        reinterpret_cast<const v4i*>(ctx + L.wcy), pp, sw, sa, gout, x, gx,
                        reinterpret_cast<float*>(ws + W.lsq_part));
     prof_end(slot, s);

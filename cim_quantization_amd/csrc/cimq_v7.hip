@@ -39,6 +39,7 @@ struct V7 {
   int NSEG;     // segments per output row
   int NRS;      // output rows per step (64 pixels)
   int RSLOT;    // ring rows (NRS + 2)
+  int NPART;    // waves sharing one pixel group (split over (c, kh)-blocks)
   // grad_x
   int RB;       // input rows owned by one block
   int nbands;   // bands per image
@@ -81,8 +82,10 @@ __device__ inline float dpp_from_prev(float v) {
 // contributing output rows are done are folded along kh, scaled, run through the LSQ act
 // backward and stored -- no atomics, every value written by exactly one lane.
 // ---------------------------------------------------------------------------------------
-template <int NBW, int NBA, int OBX, bool LSQ, int SS>
-__global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
+// NPART waves share one pixel group, each owning the (c, kh)-blocks cb = part (mod NPART): more
+// waves per image for small images, every ring value still written by exactly one lane.
+template <int NBW, int NBA, int OBX, bool LSQ, int SS, int NPART>
+__global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
                                                             const v4i* __restrict__ wcy, Params pp,
                                                             const float* __restrict__ sw_p,
                                                             const float* __restrict__ sa_p,
@@ -120,11 +123,12 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
     for (int j = 1; j < NBA; ++j) nominal = nominal && (cel[k * NBA + j] == cek[k]);
   }
   const float scale = sw / (float)NBA;
-  float part = 0.f;
+  float gpart = 0.f;
   int done = r0 - 1;
   for (int step = 0; step < nsteps; ++step) {
     const int oh_s = oh_lo + step * v.NRS, oh_e = min(oh_hi, oh_s + v.NRS - 1);
-    const int q = 16 * wave + r16;
+    const int q = 16 * (wave & 3) + r16;
+    const int part = wave >> 2;
     const int oh = oh_s + (q >> v.lw), ow = q & (Wo - 1);
     const bool pv = oh <= oh_e;
     const int pimg = (oh << v.lw) + ow;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
       const v4i* wt = wcy + (size_t)i * v.NCPBT * NKS * 64 + lane;
 #pragma unroll
       for (int cb = 0; cb < 12; ++cb) {
-        if (cb < ncb) {
+        if (cb < ncb && (NPART == 1 || (cpb_lo + cb) % NPART == part)) {
           v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < NKS; ++s) {
@@ -269,8 +273,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
           const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
           const float gy = pass ? gqv * sa : 0.f;
           gx[gi] = gy / sa;
-          part += gqv * rp;
-          part += -(gy * (y1 / sa));
+          gpart += gqv * rp;
+          gpart += -(gy * (y1 / sa));
         } else {
           gx[gi] = gqv;
         }
@@ -280,10 +284,14 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v8_kernel(Geo g, V7 v, cons
     __syncthreads();
   }
   if (LSQ) {
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) red[wave] = part;
+    for (int o = 32; o > 0; o >>= 1) gpart += __shfl_xor(gpart, o);
+    if (lane == 0) red[wave] = gpart;
     __syncthreads();
-    if (threadIdx.x == 0) gsa_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < 4 * NPART; ++w) t += red[w];
+      gsa_part[blockIdx.x] = t;
+    }
   }
 }
 
