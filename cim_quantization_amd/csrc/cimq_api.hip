@@ -229,7 +229,9 @@ Plan3 v3_plan(const Geo& g) {
   const int nkj = g.nbw * g.nba;
   const size_t ckl = a16((size_t)3 * nkj * 4);
   const size_t patch = a16((size_t)g.C * v.RH * v.WP * g.NBP);
-  const int nof = std::min(4, g.OB16), nog = std::min(2, g.OB16);
+  v.obm = tune("FWD_OBM", 2);  // two o-blocks per block (measured best for O = 32 / 64)
+  if (v.obm != 1 && v.obm != 2 && v.obm != 4) v.obm = 4;
+  const int nof = std::min(v.obm, g.OB16), nog = std::min(2, g.OB16);
   const size_t fwd_common = patch + (size_t)g.T * g.KS * 64 * 4 + ckl;
   const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * (16 + 4);
   const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
@@ -494,11 +496,12 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   // compact state words when the v7 backward will read them
   const bool cst = v7_plan(g).ok;
   // OBM: 16-channel output blocks per block (register arrays sized for exactly that)
-  auto kern = g.OB16 == 1 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 1> : cim_fwd_v3_kernel<NBP, KS, false, 1>)
-            : g.OB16 == 2 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 2> : cim_fwd_v3_kernel<NBP, KS, false, 2>)
-                          : (cst ? cim_fwd_v3_kernel<NBP, KS, true, 4> : cim_fwd_v3_kernel<NBP, KS, false, 4>);
+  const int obm = std::min(p.v.obm, g.OB16 <= 2 ? g.OB16 : 4);
+  auto kern = obm == 1 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 1> : cim_fwd_v3_kernel<NBP, KS, false, 1>)
+            : obm == 2 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 2> : cim_fwd_v3_kernel<NBP, KS, false, 2>)
+                       : (cst ? cim_fwd_v3_kernel<NBP, KS, true, 4> : cim_fwd_v3_kernel<NBP, KS, false, 4>);
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
-  dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, 4));
+  dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, obm));
   const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
                      reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);

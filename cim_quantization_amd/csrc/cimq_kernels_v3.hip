@@ -24,6 +24,7 @@ namespace cimq {
 struct V3 {
   int lw;          // log2(Wo)
   int RH;          // strip patch rows: (64/Wo - 1)*SH + KH
+  int obm;         // forward: 16-channel output blocks per block (1, 2 or 4)
   int WP;          // patch row length: W + 2*PW
   int RI, nbands;  // grad_x: owned input rows per block, bands per image
   int RHB;         // grad_x: max band patch rows
