@@ -178,9 +178,24 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
       const int cpb_lo = cp_lo >> 2, ncb = (cp_hi >> 2) - cpb_lo + 1;
       const bool shared_first = i > 0 && cpb_lo == (((i * g.xbar - 1) / 3) >> 2);
       const v4i* wt = wcy + (size_t)i * v.NCPBT * NKS * 64 + lane;
+      // this wave's (c, kh)-blocks of tile i: cb = cb0, cb0 + NPART, ...; the operand
+      // fragments of the next block are loaded while the current block's MFMAs run
+      const int cb0 = (NPART == 1) ? 0 : ((part - cpb_lo % NPART) + NPART) % NPART;
+      v4i anx[NKS];
+      if (cb0 < ncb) {
 #pragma unroll
-      for (int cb = 0; cb < 12; ++cb) {
-        if (cb < ncb && (NPART == 1 || (cpb_lo + cb) % NPART == part)) {
+        for (int s = 0; s < NKS; ++s) anx[s] = wt[(cb0 * NKS + s) * 64];
+      }
+#pragma unroll 1
+      for (int cb = cb0; cb < ncb; cb += NPART) {
+        {
+          v4i acur[NKS];
+#pragma unroll
+          for (int s = 0; s < NKS; ++s) acur[s] = anx[s];
+          if (cb + NPART < ncb) {
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) anx[s] = wt[((cb + NPART) * NKS + s) * 64];
+          }
           v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < NKS; ++s) {
@@ -188,7 +203,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
             acc[0] += (float)Gh[s][0] + (float)Gm[s][1] + (float)Gl[s][2];
             continue;
 #endif
-            const v8bf a = as_v8bf(wt[(cb * NKS + s) * 64]);
+            const v8bf a = as_v8bf(acur[s]);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gh[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gm[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gl[s], acc, 0, 0, 0);
