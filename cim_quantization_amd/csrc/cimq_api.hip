@@ -311,6 +311,12 @@ Plan7 v7_plan(const Geo& g) {
   v.NRS = 64 / g.Wo;
   if (v.NRS < 1) return p;
   v.RSLOT = v.NRS + 2;
+  // grad_x fold pass: power-of-two W and C (index math by shifts)
+  if ((g.W & (g.W - 1)) != 0 || (g.C & (g.C - 1)) != 0) return p;
+  v.lwin = 0;
+  while ((1 << v.lwin) < g.W) ++v.lwin;
+  v.lcin = 0;
+  while ((1 << v.lcin) < g.C) ++v.lcin;
   // waves per pixel group: more parallelism where an image has few pixel groups
   v.NPART = tune("GX_NPART", g.Wo >= 32 ? 1 : 2);
   if (v.NPART != 1 && v.NPART != 2 && v.NPART != 4) return p;

@@ -40,6 +40,7 @@ struct V7 {
   int NRS;      // output rows per step (64 pixels)
   int RSLOT;    // ring rows (NRS + 2)
   int NPART;    // waves sharing one pixel group (split over (c, kh)-blocks)
+  int lwin, lcin;  // log2(W), log2(C) (the v7 path takes power-of-two W and C)
   // grad_x
   int RB;       // input rows owned by one block
   int nbands;   // bands per image
@@ -261,8 +262,8 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
     if (f1 >= f0) {
       const int nf = (f1 - f0 + 1) * g.C * g.W;
       for (int t = threadIdx.x; t < nf; t += blockDim.x) {
-        const int iw = t % g.W, rest = t / g.W;
-        const int c = rest % g.C, ih = f0 + rest / g.C;
+        const int iw = t & (g.W - 1), rest = t >> v.lwin;  // power-of-two W, C (v7_plan)
+        const int c = rest & (g.C - 1), ih = f0 + (rest >> v.lcin);
         const int sg = iw / (SS * v.SWD), cl = iw - sg * (SS * v.SWD);
         float a = 0.f;
 #pragma unroll

@@ -26,6 +26,9 @@ VARIANTS = {
     "gx_nomfma": ["CIMQ_EXP_GX_NOMFMA"],
     "gx_noring": ["CIMQ_EXP_GX_NORING"],
     "fwd_nost": ["CIMQ_EXP_FWD_NOST"],
+    "gx_nofold": ["CIMQ_EXP_GX_NOFOLD"],
+    "gx_nostate": ["CIMQ_EXP_GX_NOSTATE"],
+    "gx_nofold_nomfma": ["CIMQ_EXP_GX_NOFOLD", "CIMQ_EXP_GX_NOMFMA"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
