@@ -142,7 +142,9 @@ CtxLayout ctx_layout(const Geo& g) {
   L.flags = o; o = align256(o + 16);
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
-  L.st = o; o = align256(o + std::max((size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4), (size_t)g.T * g.M * g.O * 4));
+  // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three
+  // 64-bit planes for w8a8) per (tile, pixel, channel)
+  L.st = o; o = align256(o + std::max((size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4), (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24)));
   L.lsq_scal = o; o = align256(o + 16 * 4);
   L.total = o;
   return L;
@@ -285,8 +287,11 @@ Plan7 v7_plan(const Geo& g) {
   return p;
 #endif
   const Plan3 p3 = v3_plan(g);
-  if (!p3.ok || g.NBP != 4) return p;
-  if (!((g.nbw == 3 && g.nba == 3) || (g.nbw == 2 && g.nba == 2))) return p;  // instantiated slice pairs
+  if (!p3.ok) return p;
+  // instantiated slice pairs: w3a3 / w2a2 (interleaved state words) and w8a8 (plane state words)
+  if (g.NBP == 4 && !((g.nbw == 3 && g.nba == 3) || (g.nbw == 2 && g.nba == 2))) return p;
+  // w8a8: one 16-channel output block (the first conv of the CIFAR ResNets; wider blocks spill)
+  if (g.NBP == 8 && !(g.nbw == 8 && g.nba == 8 && g.OB16 == 1)) return p;
   if (g.O % 16 != 0 || !(g.OB16 == 1 || g.OB16 == 2 || g.OB16 == 4)) return p;
   // 3x3, stride 1, pad 1 ("same" conv: every CiM conv of the CIFAR ResNets but the downsampling ones)
   if (g.KH != 3 || g.KW != 3 || g.SH != g.SW || g.SH > 2 || g.PH != 1 || g.PW != 1) return p;
@@ -311,32 +316,37 @@ Plan7 v7_plan(const Geo& g) {
   v.NRS = 64 / g.Wo;
   if (v.NRS < 1) return p;
   v.RSLOT = v.NRS + 2;
-  // grad_x fold pass: power-of-two W and C (index math by shifts)
-  if ((g.W & (g.W - 1)) != 0 || (g.C & (g.C - 1)) != 0) return p;
+  // grad_x fold pass: power-of-two W (index math by shifts); C by shifts when a power of two
+  if ((g.W & (g.W - 1)) != 0) return p;
   v.lwin = 0;
   while ((1 << v.lwin) < g.W) ++v.lwin;
   v.lcin = 0;
   while ((1 << v.lcin) < g.C) ++v.lcin;
+  if ((1 << v.lcin) != g.C) v.lcin = -1;
   // waves per pixel group: more parallelism where an image has few pixel groups
   v.NPART = tune("GX_NPART", g.Wo >= 32 ? 1 : 2);
   if (v.NPART != 1 && v.NPART != 2 && v.NPART != 4) return p;
+  if (g.NBP == 8 && v.NPART == 4) v.NPART = 2;  // 128-VGPR cap of 1024-thread blocks spills w8a8
   p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (g.SH * v.SWD + 2) * 4) + 64 * 4 + 64;
   // grad_w
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
   v.CPITCH = v.NSLOT * g.Wo + 8;
-  const size_t planes = (size_t)g.nba * g.KW * 16 * v.CPITCH * 2;
-  p.lds_gw = std::max(a16(planes), (size_t)4 * 9 * 256 * 4) + 64 * 4 + (size_t)4 * 3 * g.nbw * g.nba * 16 * 4;
-  if (g.SH == 1 && 16 * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
+  v.CPL = std::min(16, g.C);
+  // tiles touching one channel block (the kernel's loop takes at most 3)
+  v.NTL = 1;
+  for (int cb = 0; cb * 16 < g.C; ++cb) {
+    const int ilo = (cb * 16 * g.KHW) / g.xbar, ihi = (std::min(g.C, cb * 16 + 16) * g.KHW - 1) / g.xbar;
+    v.NTL = std::max(v.NTL, ihi - ilo + 1);
+  }
+  if (v.NTL > 3) return p;
+  const size_t planes = (size_t)g.nba * g.KW * v.CPL * v.CPITCH * 2;
+  p.lds_gw = std::max(a16(planes), (size_t)4 * 9 * 256 * 4) + 64 * 4 + (size_t)4 * v.NTL * g.nbw * g.nba * 16 * 4;
+  if (g.SH == 1 && v.CPL * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
   p.pairs = ((g.C + 15) / 16) * g.OB16;
   const int stages = g.M / 128;
   const int want = std::max(1, tune("GW_BLOCKS", 512) / p.pairs);
   v.nstage = std::max(1, (stages + want - 1) / want);
   v.nchunks = (stages + v.nstage - 1) / v.nstage;
-  // tiles touching one channel block (register arrays sized for 4)
-  for (int cb = 0; cb * 16 < g.C; ++cb) {
-    const int ilo = (cb * 16 * g.KHW) / g.xbar, ihi = (std::min(g.C, cb * 16 + 16) * g.KHW - 1) / g.xbar;
-    if (ihi - ilo + 1 > 3) return p;
-  }
   const size_t lim = kLdsMax - 512;
   p.ok = p.lds_gx <= lim && p.lds_gw <= lim;
   return p;
@@ -677,9 +687,13 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
 template <int NBW, int NBA>
 int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq) {
-  if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
-  if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
-  return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+  if constexpr (NBW * NBA > 10) {
+    return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);  // v7_plan: OB16 == 1
+  } else {
+    if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+    if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+    return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+  }
 }
 
 template <int NBP, int FBMAX>
@@ -690,6 +704,7 @@ int launch_bwd_all(const Geo& g, const uint8_t* ctx, const float* sw, const floa
   if (p7.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
+    if (NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
     if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
     return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
   }

@@ -375,6 +375,14 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       for (int a = 0; a < OBM; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) stc[a][c] = 0u;
+      // plane state words (more than 10 slice pairs, NBP 8): per (i, m, o) three 64-bit planes
+      // -- STE pass, code != 0, code < 0 -- bit k*nba + j each (cimq_v7.hip)
+      constexpr bool PLF = (NBP == 8) && CST;
+      uint64_t pl[OBM][4][3];
+#pragma unroll
+      for (int a = 0; a < OBM; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pl[a][c][0] = pl[a][c][1] = pl[a][c][2] = 0ull;
       for (int k = 0; k < g.nbw; ++k) {
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
@@ -384,6 +392,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) wk[ks] = wt[((k * NOB + ob) * KS + ks) * 64 + lane];
             uint32_t stw[4] = {0u, 0u, 0u, 0u};
+            uint32_t tq[4][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}};
 #pragma unroll
             for (int j = 0; j < NBP; ++j) {
               if (j < g.nba) {
@@ -401,7 +410,13 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                     a = lo ? -cf : a;
                     acc[ob][r] += a;
                     const bool pass = (unsigned)(ps[r] - pv.z) <= (unsigned)pv.w;
-                    stw[r] |= ((pass ? 1u : 0u) | ((hi || lo) ? 2u : 0u) | (lo ? 4u : 0u)) << (3 * j);
+                    if (PLF) {
+                      tq[r][0] |= (pass ? 1u : 0u) << j;
+                      tq[r][1] |= ((hi || lo) ? 1u : 0u) << j;
+                      tq[r][2] |= (lo ? 1u : 0u) << j;
+                    } else {
+                      stw[r] |= ((pass ? 1u : 0u) | ((hi || lo) ? 2u : 0u) | (lo ? 4u : 0u)) << (3 * j);
+                    }
                   }
                 } else {
                   const float al = pp.alpha[pidx(g, i, j, k, o)];
@@ -414,12 +429,24 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                                                : ((unsigned)(ps[r] - pv.z) <= (unsigned)pv.w);
                     const float code =
                         has_code ? code_literal(ps[r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo) : 0.f;
-                    stw[r] |= st_bits(pass, code) << (3 * j);
+                    const uint32_t sb = st_bits(pass, code);
+                    if (PLF) {
+                      tq[r][0] |= (sb & 1u) << j;
+                      tq[r][1] |= ((sb >> 1) & 1u) << j;
+                      tq[r][2] |= ((sb >> 2) & 1u) << j;
+                    } else {
+                      stw[r] |= sb << (3 * j);
+                    }
                   }
                 }
               }
             }
-            if (CST) {
+            if (PLF) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) pl[ob][r][q] |= (uint64_t)tq[r][q] << (g.nba * k);
+            } else if (CST) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) stc[ob][r] |= stw[r] << (3 * g.nba * k);
             }
@@ -444,9 +471,19 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #else
           if (ob < nob && o < g.O) {
 #endif
-            uint32_t* s32 = reinterpret_cast<uint32_t*>(st) + ((size_t)i * g.M + (size_t)mt * 64 + wave * 16 + 4 * g4) * g.O + o;
+            const size_t e0 = ((size_t)i * g.M + (size_t)mt * 64 + wave * 16 + 4 * g4) * g.O + o;
+            if (PLF) {
+              uint2* s64 = reinterpret_cast<uint2*>(st);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stc[ob][r];
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                  s64[(e0 + (size_t)r * g.O) * 3 + q] = make_uint2((uint32_t)pl[ob][r][q], (uint32_t)(pl[ob][r][q] >> 32));
+            } else {
+              uint32_t* s32 = reinterpret_cast<uint32_t*>(st) + e0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stc[ob][r];
+            }
           }
         }
       }

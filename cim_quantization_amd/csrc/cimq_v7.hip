@@ -27,6 +27,8 @@
 // Both replace the state-word (16-bit per (i, k, quad, o)) kernels of cimq_kernels_v3.hip /
 // cimq_gx_v6.hip on layers the v7 plan accepts (host: v7_plan in cimq_api.hip).
 #pragma once
+#include <type_traits>
+
 #include "cimq_gx_v6.hip"
 
 namespace cimq {
@@ -51,6 +53,8 @@ struct V7 {
   int nstage;   // 128-pixel stages per chunk
   int nchunks;  // pixel chunks
   int whole;    // 1: a stage is 128/P whole images; 0: a stage is 128/Wo rows of one image
+  int CPL;      // channels per staged plane: min(16, C)
+  int NTL;      // most crossbar tiles touching one 16-channel block (grad_alpha LDS regions)
 };
 
 // pass-bit masks of the state word: all j of slice k / all k of slice j
@@ -95,6 +99,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
                                                             float* __restrict__ gsa_part) {
   constexpr int NKS = (NBW * OBX + 1) / 2;
   constexpr int NKJ = NBW * NBA;
+  constexpr bool PLS = NKJ > 10;  // plane state words (cim_fwd_v3_kernel PLF)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
   const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB);
@@ -145,12 +150,27 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
         gv[ob][r] = pv ? (g.onchw ? gout[((size_t)b * g.O + o) * g.P + pimg] : gout[m * g.O + o]) : 0.f;
       }
     for (int i = 0; i < g.T; ++i) {
+      // state words of this lane's pixel, channels 4*g4 .. +3 of each o-block: interleaved
+      // (3 bits per slice pair) or, for more than 10 pairs, the 64-bit pass plane
       uint32_t sv[OBX][4];
+      uint64_t sp[OBX][4];
 #pragma unroll
       for (int ob = 0; ob < OBX; ++ob) {
-        uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
-        if (pv) s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + ob * 16 + 4 * g4);
-        sv[ob][0] = s4.x; sv[ob][1] = s4.y; sv[ob][2] = s4.z; sv[ob][3] = s4.w;
+        if constexpr (PLS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            uint2 w2 = make_uint2(0u, 0u);
+            if (pv) w2 = reinterpret_cast<const uint2*>(st)[(((size_t)i * g.M + m) * g.O + ob * 16 + 4 * g4 + r) * 3];
+            sp[ob][r] = (uint64_t)w2.x | ((uint64_t)w2.y << 32);
+            sv[ob][r] = 0u;
+          }
+        } else {
+          uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
+          if (pv) s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + ob * 16 + 4 * g4);
+          sv[ob][0] = s4.x; sv[ob][1] = s4.y; sv[ob][2] = s4.z; sv[ob][3] = s4.w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sp[ob][r] = 0ull;
+        }
       }
       v8bf Gh[NKS], Gm[NKS], Gl[NKS];
 #pragma unroll
@@ -163,7 +183,16 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
           if (kb < NBW * OBX) {
             const int k = kb / OBX, ob = kb - k * OBX;
             float E;
-            if (nominal) {
+            if constexpr (PLS) {
+              const uint32_t fld = (uint32_t)(sp[ob][r] >> (k * NBA)) & ((1u << NBA) - 1u);
+              if (nominal) {
+                E = cek[k] * (float)__popc(fld);
+              } else {
+                E = 0.f;
+#pragma unroll
+                for (int j = 0; j < NBA; ++j) E += ((fld >> j) & 1u) ? cel[k * NBA + j] : 0.f;
+              }
+            } else if (nominal) {
               E = cek[k] * (float)__popc(sv[ob][r] & pass_mask_k(k, NBA));
             } else {
               E = 0.f;
@@ -262,8 +291,9 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
     if (f1 >= f0) {
       const int nf = (f1 - f0 + 1) * g.C * g.W;
       for (int t = threadIdx.x; t < nf; t += blockDim.x) {
-        const int iw = t & (g.W - 1), rest = t >> v.lwin;  // power-of-two W, C (v7_plan)
-        const int c = rest & (g.C - 1), ih = f0 + (rest >> v.lcin);
+        const int iw = t & (g.W - 1), rest = t >> v.lwin;  // power-of-two W (v7_plan)
+        const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
+        const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
         const int sg = iw / (SS * v.SWD), cl = iw - sg * (SS * v.SWD);
         float a = 0.f;
 #pragma unroll
@@ -478,6 +508,33 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gx_v7_kernel(Geo g, V7 v, cons
 // block = (pixel chunk, (channel block cb, output block ob)); a chunk is nstage stages of 128
 // output pixels; in a stage wave w owns the 32 pixels 32w..32w+31 (one MFMA K-step).
 // stride 1 (v7_plan); at most 3 crossbar tiles touch one 16-channel block.
+// ctx slice bytes of one input element: NBP = 4 (uint32) or 8 (uint2) bytes, slice j in byte j
+__device__ inline uint32_t xbyte(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
+__device__ inline uint32_t xbyte(uint2 w, int j) { return (j < 4 ? (w.x >> (8 * j)) : (w.y >> (8 * (j - 4)))) & 0xFFu; }
+template <typename XW>
+__device__ inline XW xzero();
+template <>
+__device__ inline uint32_t xzero<uint32_t>() { return 0u; }
+template <>
+__device__ inline uint2 xzero<uint2>() { return make_uint2(0u, 0u); }
+// n consecutive elements from a 16-B aligned source by 16-B loads
+template <int N>
+__device__ inline void xload(const uint32_t* src, uint32_t* d) {
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    const uint4 t = reinterpret_cast<const uint4*>(src)[q];
+    d[4 * q] = t.x; d[4 * q + 1] = t.y; d[4 * q + 2] = t.z; d[4 * q + 3] = t.w;
+  }
+}
+template <int N>
+__device__ inline void xload(const uint2* src, uint2* d) {
+#pragma unroll
+  for (int q = 0; q < N / 2; ++q) {
+    const uint4 t = reinterpret_cast<const uint4*>(src)[q];
+    d[2 * q] = make_uint2(t.x, t.y); d[2 * q + 1] = make_uint2(t.z, t.w);
+  }
+}
+
 template <int NBW, int NBA, int SS>
 __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
                                                             const uint8_t* __restrict__ xcb, Params pp,
@@ -485,8 +542,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
                                                             float* __restrict__ gw_slab,
                                                             float* __restrict__ ga_slab) {
   constexpr int NKJ = NBW * NBA;
+  constexpr bool PLS = NKJ > 10;  // plane state words (cim_fwd_v3_kernel PLF)
+  typedef typename std::conditional<(NBA > 4), uint2, uint32_t>::type XW;  // ctx slice bytes (NBP)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int chunk = blockIdx.x, pair = blockIdx.y;
+  const int CPL = v.CPL, NTL = v.NTL;
   const int cb = pair / g.OB16, ob = pair - cb * g.OB16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -500,11 +560,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   const int i_hi = (min(g.C, cb * 16 + 16) * KHW - 1) / g.xbar;
   const int ntl = i_hi - i_lo + 1;
 
-  const size_t plane = (size_t)16 * v.CPITCH;  // one (j, kw) plane, bf16 elements
+  const size_t plane = (size_t)CPL * v.CPITCH;  // one (j, kw) plane, bf16 elements
   uint8_t* cur = smem;
   __bf16* pl = reinterpret_cast<__bf16*>(cur); { const size_t pb = (size_t)NBA * 3 * plane * 2; cur += al16(pb > 36864 ? pb : (size_t)36864); }
   float* cdl = reinterpret_cast<float*>(cur); cur += 64 * 4;
-  float* red = reinterpret_cast<float*>(cur);  // [4 waves][3][NKJ][16] grad_alpha partials
+  float* red = reinterpret_cast<float*>(cur);  // [4 waves][NTL][NKJ][16] grad_alpha partials
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
   __syncthreads();
   // nominal binary mask: cD_kj independent of k, so D_j = cD_0j * popcount(pass bits of j)
@@ -526,15 +586,15 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp) acc[tp] = v4f{0.f, 0.f, 0.f, 0.f};
   // grad_alpha partials accumulate in LDS, one region per wave: red[wave][tl][kj][16 o]
-  for (int t = threadIdx.x; t < 4 * 3 * NKJ * 16; t += blockDim.x) red[t] = 0.f;
+  for (int t = threadIdx.x; t < 4 * NTL * NKJ * 16; t += blockDim.x) red[t] = 0.f;
 
   // Software pipeline over the chunk's stages: the global loads of stage n+1 (source words of
   // the staged rows, state words and grad_out of this lane's K-step) are issued before the
   // MFMA work of stage n, so their latency hides behind it.
   const int ng8 = Wo >> 3;
-  const int nit = 16 * v.NSLOT * ng8;  // staging items (<= 2 per thread, v7_plan)
+  const int nit = CPL * v.NSLOT * ng8;  // staging items (<= 2 per thread, v7_plan)
   struct Pref {
-    uint32_t w[2][10];
+    XW w[2][10];
   };
   auto stage_geom = [&](int stg, int& b0, int& ih_first) {
     const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
@@ -550,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     for (int u2 = 0; u2 < 2; ++u2) {
       const int it = threadIdx.x + u2 * 256;
 #pragma unroll
-      for (int u = 0; u < 10; ++u) pf.w[u2][u] = 0u;
+      for (int u = 0; u < 10; ++u) pf.w[u2][u] = xzero<XW>();
       if (it < nit) {
         const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
         const int slot = rem / ng8, c8 = rem - slot * ng8;
@@ -558,10 +618,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
         const int c = cb * 16 + cl;
         if (c < g.C && ih >= 0 && ih < g.H && b < g.B) {
-          const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 8;
-          const uint4 lo = reinterpret_cast<const uint4*>(src)[0], hi = reinterpret_cast<const uint4*>(src)[1];
-          pf.w[u2][1] = lo.x; pf.w[u2][2] = lo.y; pf.w[u2][3] = lo.z; pf.w[u2][4] = lo.w;
-          pf.w[u2][5] = hi.x; pf.w[u2][6] = hi.y; pf.w[u2][7] = hi.z; pf.w[u2][8] = hi.w;
+          const XW* src = reinterpret_cast<const XW*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 8;
+          xload<8>(src, &pf.w[u2][1]);
           if (c8 > 0) pf.w[u2][0] = src[-1];
           if (c8 * 8 + 8 < g.W) pf.w[u2][9] = src[8];
         }
@@ -583,16 +641,12 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         int b = b0, ih = ih_first + slot;
         if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
         const int c = cb * 16 + cl;
-        uint32_t wv[17];
+        XW wv[17];
 #pragma unroll
-        for (int u = 0; u < 17; ++u) wv[u] = 0u;
+        for (int u = 0; u < 17; ++u) wv[u] = xzero<XW>();
         if (c < g.C && ih >= 0 && ih < g.H && b < g.B) {
-          const uint32_t* src = reinterpret_cast<const uint32_t*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 16;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint4 t4 = reinterpret_cast<const uint4*>(src)[q];
-            wv[1 + 4 * q] = t4.x; wv[2 + 4 * q] = t4.y; wv[3 + 4 * q] = t4.z; wv[4 + 4 * q] = t4.w;
-          }
+          const XW* src = reinterpret_cast<const XW*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 16;
+          xload<16>(src, &wv[1]);
           if (c8 > 0) wv[0] = src[-1];
         }
 #pragma unroll
@@ -602,12 +656,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             uint32_t pk[4];
 #pragma unroll
             for (int e2 = 0; e2 < 4; ++e2) {
-              const uint32_t w0 = wv[4 * e2 + kw], w1 = wv[4 * e2 + 2 + kw];
-              const float f0 = (float)(int8_t)((w0 >> (8 * j)) & 0xFFu);
-              const float f1 = (float)(int8_t)((w1 >> (8 * j)) & 0xFFu);
+              const float f0 = (float)(int8_t)xbyte(wv[4 * e2 + kw], j);
+              const float f1 = (float)(int8_t)xbyte(wv[4 * e2 + 2 + kw], j);
               pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
             }
-            __bf16* dst = pl + ((size_t)(j * 3 + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            __bf16* dst = pl + ((size_t)(j * 3 + kw) * CPL + cl) * v.CPITCH + slot * Wo + c8 * 8;
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
@@ -632,12 +685,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             uint32_t pk[4];
 #pragma unroll
             for (int e2 = 0; e2 < 4; ++e2) {
-              const uint32_t w0 = pf.w[u2][2 * e2 + kw], w1 = pf.w[u2][2 * e2 + 1 + kw];
-              const float f0 = (float)(int8_t)((w0 >> (8 * j)) & 0xFFu);
-              const float f1 = (float)(int8_t)((w1 >> (8 * j)) & 0xFFu);
+              const float f0 = (float)(int8_t)xbyte(pf.w[u2][2 * e2 + kw], j);
+              const float f1 = (float)(int8_t)xbyte(pf.w[u2][2 * e2 + 1 + kw], j);
               pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);  // exact bf16
             }
-            __bf16* dst = pl + ((size_t)(j * 3 + kw) * 16 + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            __bf16* dst = pl + ((size_t)(j * 3 + kw) * CPL + cl) * v.CPITCH + slot * Wo + c8 * 8;
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
@@ -672,7 +724,81 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     }
 #pragma unroll 1
     for (int tl = 0; tl < 3; ++tl) {
-      if (tl < ntl) {
+      if (PLS && tl < ntl) {
+        // plane state words: grad_alpha from the code planes, then one slice j at a time
+        const int i = i_lo + tl;
+        const uint2* s2 = reinterpret_cast<const uint2*>(st) + ((size_t)i * g.M + mk8) * g.O * 3 + (size_t)o * 3;
+        const size_t es = (size_t)g.O * 3;
+        if (((i * g.xbar) / KHW) / 16 == cb) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t nzw[8], ngw[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const uint2 a = s2[e * es + 1], c2 = s2[e * es + 2];
+              nzw[e] = h ? a.y : a.x;
+              ngw[e] = h ? c2.y : c2.x;
+            }
+#pragma unroll
+            for (int kk = 0; kk < 32; ++kk) {
+              const int kj = 32 * h + kk;
+              if (kj < NKJ) {
+                float q = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  const uint32_t nzm = (uint32_t)(((int)(nzw[e] << (31 - kk))) >> 31);
+                  const uint32_t sgn = (ngw[e] << (31 - kk)) & 0x80000000u;
+                  q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
+                }
+                q += __shfl_xor(q, 16);
+                q += __shfl_xor(q, 32);
+                if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
+              }
+            }
+          }
+        }
+        uint64_t ps[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint2 a = s2[e * es];
+          ps[e] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        }
+        const int rowc = r16 < CPL ? r16 : 0;
+#pragma unroll 1
+        for (int j = 0; j < NBA; ++j) {
+          uint64_t mj = 0ull;
+#pragma unroll
+          for (int k = 0; k < NBW; ++k) mj |= 1ull << (k * NBA + j);
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float D;
+            if (nominal) {
+              D = cdl[j] * (float)__popcll(ps[e] & mj);
+            } else {
+              D = 0.f;
+#pragma unroll
+              for (int k = 0; k < NBW; ++k) D += ((ps[e] >> (k * NBA + j)) & 1ull) ? cdl[k * NBA + j] : 0.f;
+            }
+            d[e] = gv[e] * D;
+          }
+          v8bf bh, bm, bq;
+          split3x8(d, bh, bm, bq);
+#pragma unroll
+          for (int tp = 0; tp < 9; ++tp) {
+            const int kh = tp / 3, kw = tp - 3 * (tp / 3);
+            const int sl = slot_kh[kh];
+            const bool ok = (tit[tp] == i) && sl >= 0;
+            const __bf16* src = pl + ((size_t)(j * 3 + kw) * CPL + rowc) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
+            v4i a4 = *reinterpret_cast<const v4i*>(src);
+            a4 = ok ? a4 : v4i{0, 0, 0, 0};
+            const v8bf a = as_v8bf(a4);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[tp], 0, 0, 0);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[tp], 0, 0, 0);
+            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[tp], 0, 0, 0);
+          }
+        }
+      } else if (!PLS && tl < ntl) {
         const int i = i_lo + tl;
         uint32_t sv[8];
 #pragma unroll
@@ -695,7 +821,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             }
             q += __shfl_xor(q, 16);
             q += __shfl_xor(q, 32);
-            if (g4 == 0) red[((wave * 3 + tl) * NKJ + kj) * 16 + r16] += q;
+            if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
           }
         }
         // B operands: g * D_j, D_j = sum_k cD_kj * pass_ijk, split into bf16 hi / mid / lo
@@ -723,10 +849,10 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           const int kh = tp / 3, kw = tp - 3 * (tp / 3);
           const int sl = slot_kh[kh];
           const bool ok = (tit[tp] == i) && sl >= 0;
-          const __bf16* src = pl + ((size_t)kw * 16 + r16) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
+          const __bf16* src = pl + ((size_t)kw * CPL + (r16 < CPL ? r16 : 0)) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
 #pragma unroll
           for (int j = 0; j < NBA; ++j) {
-            const v4i a = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * 16 * v.CPITCH);
+            const v4i a = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * CPL * v.CPITCH);
             dst[j] = ok ? a : v4i{0, 0, 0, 0};
           }
         };
@@ -772,7 +898,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     const int tl = t / (NKJ * 16), rem = t - tl * NKJ * 16, kj = rem >> 4, oc = rem & 15;
     const int i = i_lo + tl;
     if (((i * g.xbar) / KHW) / 16 == cb) {
-      const int w1 = 3 * NKJ * 16;
+      const int w1 = NTL * NKJ * 16;
       const float sum = (red[t] + red[w1 + t]) + (red[2 * w1 + t] + red[3 * w1 + t]);
       ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + ob * 16 + oc] = sum;
     }

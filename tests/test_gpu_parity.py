@@ -112,6 +112,10 @@ RANDOM_CASES = [
     dict(B=2, C=32, O=32, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
     dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=2, ab=2, wbs=1, abs=1, xbar=64, adc=1.5, signed=0),
     dict(B=2, C=32, O=16, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=64, adc=4, signed=0),
+    # w8a8 on the v7 backward (64 slice pairs: plane state words): the first conv, a 2-tile case
+    dict(B=2, C=3, O=16, H=32, k=3, s=1, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=1),
+    dict(B=2, C=3, O=16, H=16, k=3, s=2, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=1),
+    dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
     # sign ADC: sign(ps) at ps = 0 follows the reference's fp32 residues (slice artifacts,
     # summation order), so this case uses power-of-two scales: x_int, w_int exact
     dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1, signed=0, sa=0.125,
