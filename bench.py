@@ -41,7 +41,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
 TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r01_v9", "pmc_traffic.json"))
 # rocprof symbol of each v7-path kernel id (the names pmc_traffic.json is keyed by)
-V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, true>", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
+V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, 3, ", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
               "gw_v7": "cimq::cim_bwd_gw_v7_kernel<3, 3>"}
 
 

@@ -513,9 +513,20 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   const bool cst = v7_plan(g).ok;
   // OBM: 16-channel output blocks per block (register arrays sized for exactly that)
   const int obm = std::min(p.v.obm, g.OB16 <= 2 ? g.OB16 : 4);
-  auto kern = obm == 1 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 1> : cim_fwd_v3_kernel<NBP, KS, false, 1>)
-            : obm == 2 ? (cst ? cim_fwd_v3_kernel<NBP, KS, true, 2> : cim_fwd_v3_kernel<NBP, KS, false, 2>)
-                       : (cst ? cim_fwd_v3_kernel<NBP, KS, true, 4> : cim_fwd_v3_kernel<NBP, KS, false, 4>);
+  // CST: compact state words with nbw = nba = CST fixed at compile time (v7_plan's slice pairs)
+  void (*kern)(Geo, V3, const uint8_t*, const v4i*, Params, const float*, const float*, float*, uint8_t*);
+  if (!cst) {
+    kern = obm == 1 ? cim_fwd_v3_kernel<NBP, KS, 0, 1> : obm == 2 ? cim_fwd_v3_kernel<NBP, KS, 0, 2>
+                                                       : cim_fwd_v3_kernel<NBP, KS, 0, 4>;
+  } else if constexpr (NBP == 8) {
+    kern = cim_fwd_v3_kernel<8, KS, 8, 1>;  // v7_plan: w8a8 with one 16-channel block
+  } else if (g.nbw == 2) {
+    kern = obm == 1 ? cim_fwd_v3_kernel<NBP, KS, 2, 1> : obm == 2 ? cim_fwd_v3_kernel<NBP, KS, 2, 2>
+                                                       : cim_fwd_v3_kernel<NBP, KS, 2, 4>;
+  } else {
+    kern = obm == 1 ? cim_fwd_v3_kernel<NBP, KS, 3, 1> : obm == 2 ? cim_fwd_v3_kernel<NBP, KS, 3, 2>
+                                                       : cim_fwd_v3_kernel<NBP, KS, 3, 4>;
+  }
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
   dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, obm));
   const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);

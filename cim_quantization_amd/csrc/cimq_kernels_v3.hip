@@ -277,9 +277,28 @@ __device__ inline uint32_t st_bits(bool pass, float code) {
   return (pass ? 1u : 0u) | ((code != 0.f) ? 2u : 0u) | ((code < 0.f) ? 4u : 0u);
 }
 
+// shift a bit in: x * 2 + c in one v_addc_co_u32 whose carry-in is the compare's lane mask
+// (the compiler spends a cndmask + shift/or on the plain expression)
+__device__ inline uint32_t shin(uint32_t x, uint64_t m) {
+  uint32_t r;
+  uint64_t co;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(x), "s"(m));
+  return r;
+}
+// ternary ADC term: hi ? cf : (lo ? -cf : 0) from the two compare masks (two cndmasks; the
+// plain expression makes the compiler rematerialise the masks as 0/1 vectors)
+__device__ inline float adc3(float cf, uint64_t mhi, uint64_t mlo) {
+  float a, r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(a) : "v"(cf), "s"(mhi));
+  asm("v_cndmask_b32_e64 %0, %1, -%2, %3" : "=v"(r) : "v"(a), "v"(cf), "s"(mlo));
+  return r;
+}
+
 // CST: compact state words (cimq_v7.hip) -- one uint32 per (tile i, pixel m, channel o) at
 // st32[(i*M + m)*O + o], bits 3*(k*nba + j) + {0: STE pass, 1: code != 0, 2: code < 0}.
-template <int NBP, int KS, bool CST, int OBM>
+// CST > 0 also fixes nbw = nba = CST at compile time: the ternary-threshold path then runs
+// fully unrolled (every slice pair's MFMAs issued before its ADC work, state bits shifted in).
+template <int NBP, int KS, int CST, int OBM>
 __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
@@ -338,8 +357,10 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 
   for (int i = 0; i < g.T; ++i) build_ptab(g, i, KS, v.RH, v.WP, ptab + i * KS * 64);
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
+#ifndef CIMQ_EXP_FWD_NOPRO
   if (v.fwd_res)
     for (int i = 0; i < g.T; ++i) stage_tile(i, i);
+#endif
   zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * v.RH * v.WP * NBP / 4);
 
   const int pl = wave * 16 + r16;  // this lane's gather pixel within the m-tile
@@ -350,7 +371,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     const int b = mt / tiles_per_img, p0 = (mt - b * tiles_per_img) * 64;
     const int oh0 = p0 >> v.lw;
     __syncthreads();
+#ifndef CIMQ_EXP_FWD_NOSTAGE
     stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
+#endif
     __syncthreads();
     float acc[OBM][4];
 #pragma unroll
@@ -366,7 +389,12 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const int tt = v.fwd_res ? i : 0;
       const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;  // K-steps holding data in tile i
       v4i xs[NBP][KS];
-      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, ksn);
+      // (the fast path runs every K-step: ptab and the weight operand are zero past the tile)
+#ifdef CIMQ_EXP_FWD_NOGATHER
+      for (int a = 0; a < NBP; ++a) for (int c = 0; c < KS; ++c) xs[a][c] = v4i{lane, a, c, i};
+#else
+      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, (CST > 0 && !literal) ? KS : ksn);
+#endif
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
       const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
@@ -383,7 +411,77 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       for (int a = 0; a < OBM; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) pl[a][c][0] = pl[a][c][1] = pl[a][c][2] = 0ull;
-      for (int k = 0; k < g.nbw; ++k) {
+      if (CST > 0 && !literal) {
+        // fast path: slice pairs kj = k*CST + j in descending order, so that shifting each
+        // state bit in from the bottom leaves bit 3*kj + {0,1,2} (interleaved words) or bit
+        // kj of each 64-bit plane (PLF) where cimq_v7.hip reads it
+        constexpr int NS = CST > 0 ? CST : 1;
+        uint32_t sw3[OBM][4][PLF ? 6 : 1];
+#pragma unroll
+        for (int a = 0; a < OBM; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int q = 0; q < (PLF ? 6 : 1); ++q) sw3[a][c][q] = 0u;
+#pragma unroll
+        for (int k = NS - 1; k >= 0; --k) {
+#pragma unroll
+          for (int ob = 0; ob < OBM; ++ob) {
+            if (ob < nob) {
+              v4i wk[KS];
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) wk[ks] = wt[((k * NOB + ob) * KS + ks) * 64 + lane];
+              v4i ps[NS];
+#pragma unroll
+              for (int j = 0; j < NS; ++j) {
+                ps[j] = v4i{0, 0, 0, 0};
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+              }
+#pragma unroll
+              for (int j = NS - 1; j >= 0; --j) {
+                const int pcol = (j * NS + k) * NOB * 16 + ob * 16 + r16;
+                const int4 pv = pt[pcol];
+                const float cf = ct[pcol];
+                const int kj = k * NS + j;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+#ifdef CIMQ_EXP_FWD_NOADC
+                  acc[ob][r] += (float)ps[j][r] * cf;
+                  continue;
+#endif
+                  const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
+                  const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
+                  const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(ps[j][r] - pv.z) <= (unsigned)pv.w);
+                  const uint64_t mnz = mhi | mlo;
+                  acc[ob][r] += adc3(cf, mhi, mlo);
+                  if constexpr (PLF) {
+                    const int wd = kj >= 32 ? 1 : 0;
+                    sw3[ob][r][wd] = shin(sw3[ob][r][wd], mps);
+                    sw3[ob][r][2 + wd] = shin(sw3[ob][r][2 + wd], mnz);
+                    sw3[ob][r][4 + wd] = shin(sw3[ob][r][4 + wd], mlo);
+                  } else {
+                    sw3[ob][r][0] = shin(shin(shin(sw3[ob][r][0], mlo), mnz), mps);
+                  }
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < OBM; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (PLF) {
+#pragma unroll
+              for (int q = 0; q < 3; ++q)
+                pl[a][c][q] = (uint64_t)sw3[a][c][2 * q] | ((uint64_t)sw3[a][c][2 * q + 1] << 32);
+            } else {
+              stc[a][c] = sw3[a][c][0];
+            }
+          }
+      }
+      for (int k = 0; k < ((CST > 0 && !literal) ? 0 : g.nbw); ++k) {
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
           if (ob < nob) {

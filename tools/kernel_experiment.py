@@ -29,6 +29,10 @@ VARIANTS = {
     "gx_nofold": ["CIMQ_EXP_GX_NOFOLD"],
     "gx_nostate": ["CIMQ_EXP_GX_NOSTATE"],
     "gx_nofold_nomfma": ["CIMQ_EXP_GX_NOFOLD", "CIMQ_EXP_GX_NOMFMA"],
+    "fwd_noadc": ["CIMQ_EXP_FWD_NOADC"],
+    "fwd_nopro": ["CIMQ_EXP_FWD_NOPRO"],
+    "fwd_nostage": ["CIMQ_EXP_FWD_NOSTAGE"],
+    "fwd_nogather": ["CIMQ_EXP_FWD_NOGATHER"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
