@@ -205,6 +205,7 @@ Plan3 v3_plan(const Geo& g) {
   if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0 || g.Wo < 4) return p;
   if (g.O > 256 || 256 % g.O != 0) return p;  // grad_alpha reducer: one thread per channel
   if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
+  if (g.M >= (1 << 24)) return p;  // float-reciprocal index division (fdiv) in the kernels
   V3& v = p.v;
   v.lw = 0;
   while ((1 << v.lw) < g.Wo) ++v.lw;

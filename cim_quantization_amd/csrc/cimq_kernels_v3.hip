@@ -173,8 +173,8 @@ __device__ inline void build_ptab(const Geo& g, int i, int KSx, int RHx, int WP,
     const int f = i * g.xbar + t;
     int off = 0;
     if (t < g.xbar && f < g.K) {
-      const int c = f / g.KHW, rem = f - c * g.KHW;
-      const int kh = rem / g.KW, kw = rem - kh * g.KW;
+      const int c = fdiv(f, g.KHW, 1.f / (float)g.KHW), rem = f - c * g.KHW;
+      const int kh = fdiv(rem, g.KW, 1.f / (float)g.KW), kw = rem - kh * g.KW;
       off = ((c - c0) * RHx + kh) * WP + kw;
     }
     ptab[t] = off;
@@ -328,17 +328,23 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   const int Wo = 1 << v.lw;
   const size_t MQ = (size_t)g.M >> 2;
 
+  // index math by shifts (NOB in {1, 2, 4}, KS in {1, 2}) and a float-reciprocal division
+  // by nbw: integer division is ~30 VALU each, and this prologue runs once per block
+  const int lnob = NOB == 4 ? 2 : NOB - 1;
+  const float inv_nbw = 1.f / (float)g.nbw;
   auto stage_tile = [&](int i, int tt) {
     batched_copy<4>(g.nbw * NOB * KS * 64, wfl + (size_t)tt * g.nbw * NOB * KS * 64, [&](int idx) -> v4i {
       const int l = idx & 63, fr = idx >> 6;
-      const int ks = fr % KS, kob = fr / KS, k = kob / NOB, ob = kob - k * NOB;
+      const int ks = KS == 1 ? 0 : (fr & 1), kob = KS == 1 ? fr : (fr >> 1);
+      const int k = kob >> lnob, ob = kob - (k << lnob);
       v4i w = {0, 0, 0, 0};
       if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
       return w;
     });
     if (!flag_lit) {
       batched_copy<2>(nkj * NOB * 16, prm + (size_t)tt * nkj * NOB * 16, [&](int idx) -> int4 {
-        const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
+        const int col = idx & ((16 << lnob) - 1), jk = idx >> (4 + lnob);
+        const int j = fdiv(jk, g.nbw, inv_nbw), k = jk - j * g.nbw;
         const int o = og * OBM * 16 + col;
         int4 p = make_int4(0, 0, 0, 0);
         if (o < g.Opad) {
@@ -348,7 +354,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
         return p;
       });
       batched_copy<4>(nkj * NOB * 16, cfl + (size_t)tt * nkj * NOB * 16, [&](int idx) -> float {
-        const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
+        const int col = idx & ((16 << lnob) - 1), jk = idx >> (4 + lnob);
+        const int j = fdiv(jk, g.nbw, inv_nbw), k = jk - j * g.nbw;
         const int o = og * OBM * 16 + col;
         return (o < g.Opad) ? pp.coef[pidx(g, i, j, k, o)] : 0.f;
       });
@@ -367,8 +374,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   const int rb = ((pl >> v.lw) * g.SH) * v.WP + (pl & (Wo - 1)) * g.SW;
   const int tiles_per_img = g.P >> 6;
 
+  const float inv_tpi = 1.f / (float)tiles_per_img, inv_p = 1.f / (float)g.P;
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
-    const int b = mt / tiles_per_img, p0 = (mt - b * tiles_per_img) * 64;
+    const int b = fdiv(mt, tiles_per_img, inv_tpi), p0 = (mt - b * tiles_per_img) * 64;
     const int oh0 = p0 >> v.lw;
     __syncthreads();
 #ifndef CIMQ_EXP_FWD_NOSTAGE
@@ -595,9 +603,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
         for (int r = 0; r < 4; ++r)
           if (!g.onchw) out[((size_t)mt * 64 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[ob][r];
         if (g.onchw) {
-          const size_t m4 = (size_t)mt * 64 + wave * 16 + 4 * g4;
-          const size_t bb = m4 / g.P, pq = m4 - bb * g.P;
-          *reinterpret_cast<float4*>(out + (bb * g.O + o) * g.P + pq) =
+          const int m4 = mt * 64 + wave * 16 + 4 * g4;  // M < 2^24 (v3_plan)
+          const int bb = fdiv(m4, g.P, inv_p), pq = m4 - bb * g.P;
+          *reinterpret_cast<float4*>(out + ((size_t)bb * g.O + o) * g.P + pq) =
               make_float4(acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
         }
       }
