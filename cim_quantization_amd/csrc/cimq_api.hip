@@ -529,7 +529,9 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
                                                        : cim_fwd_v3_kernel<NBP, KS, 3, 4>;
   }
   CIMQ_TRY(set_lds(kern, p.lds_fwd));
-  dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", 2048)), cdiv(g.OB16, obm));
+  // grid: about three resident 256-thread blocks per CU (measured: 768 blocks for w3a3, 1024
+  // for the 236-VGPR w8a8 instance)
+  dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", NBP == 8 ? 1024 : 768)), cdiv(g.OB16, obm));
   const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
                      reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);

@@ -92,25 +92,39 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
   const float xi = xq / sa;
   const int xhi = to_i8_wrap(xi);
   const int mask = (1 << g.bsa) - 1;
-  const bool xi_int = (xi == rintf(xi)) && fabsf(xi) < 16777216.f;
-  const int xii = xi_int ? (int)xi : 0;
+  // forward digits without branches for |xi| < 2^23: with F = floor(m) and fr = m - F (both
+  // exact), m = xi (unsigned) or |xi| (signed, digits negated for xi < 0), the reference's
+  // chain gives digit 0 = rint((F mod 2^b) + fr) -- 2^b for the 6 - eps artifacts -- and digit
+  // j = (F >> b*j) mod 2^b (floor(floor(m) / 2^s) = floor(m / 2^s)); larger |xi| or NaN take
+  // the float chain below
+  const bool fast = fabsf(xi) < 8388608.f;
+  const float m = sgn ? fabsf(xi) : xi;
+  const float F = floorf(m);
+  const int Fi = fast ? (int)F : 0;
+  const float fr = m - F;
+  const bool negd = sgn && xi < 0.f;
 #pragma unroll
   for (int w = 0; w < NBP / 4; ++w) { fwd[w] = 0u; bwd[w] = 0u; }
 #pragma unroll
   for (int j = 0; j < NBP; ++j) {
     if (j < g.nba) {
-      int sf, sb;
       const int sh = g.bsa * j;
-      if (sgn) {
-        sb = xhi >= 0 ? ((xhi >> sh) & mask) : -(((-xhi) >> sh) & mask);
-        sf = xii >= 0 ? ((xii >> sh) & mask) : -(((-xii) >> sh) & mask);
-      } else {
-        sb = (xhi >> sh) & mask;
-        sf = (xii >> sh) & mask;
-      }
-      if (!xi_int) sf = clamp_i8(sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa));
+      const int sb = sgn ? (xhi >= 0 ? ((xhi >> sh) & mask) : -(((-xhi) >> sh) & mask)) : ((xhi >> sh) & mask);
+      int d = (j == 0) ? min((int)rintf((float)(Fi & mask) + fr), 127) : ((Fi >> sh) & mask);
+      const int sf = negd ? -d : d;
       fwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sf << (8 * (j & 3));
       bwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sb << (8 * (j & 3));
+    }
+  }
+  if (!fast) {
+#pragma unroll
+    for (int w = 0; w < NBP / 4; ++w) fwd[w] = 0u;
+#pragma unroll
+    for (int j = 0; j < NBP; ++j) {
+      if (j < g.nba) {
+        const int sf = clamp_i8(sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa));
+        fwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sf << (8 * (j & 3));
+      }
     }
   }
 }

@@ -103,12 +103,18 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
   // the few weight-side blocks go first so their latency-bound work overlaps the act stream
   const int nwblk = (int)gridDim.x - a.nact_blocks;
   if ((int)blockIdx.x >= nwblk) {
+#ifdef CIMQ_EXP_PREP_NOACT
+    return;
+#endif
     const int ab = (int)blockIdx.x - nwblk;
     const bool sgn = a.signed_act[0] != 0.f;
     act_range(g, a.x, sa, sgn, a.xcf, a.xcb, (long long)ab * blockDim.x + threadIdx.x,
               (long long)a.nact_blocks * blockDim.x);
     return;
   }
+#ifdef CIMQ_EXP_PREP_NOWT
+  return;
+#endif
   const float sw = grad_scale_value(a.alpha_w[0], q.gs_w);  // lsq.py:553-554
   ASrc as{nullptr, 1, 0.f, 0.f};
   float mx = 0.f, mn = 0.f;

@@ -814,10 +814,10 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             float q = 0.f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              // code * g as bit ops: sign <- bit 3kj+2 (code < 0), mask <- bit 3kj+1 (code != 0)
-              const uint32_t nzm = (uint32_t)(((int)(sv[e] << (30 - 3 * kj))) >> 31);
-              const uint32_t sgn = (sv[e] << (29 - 3 * kj)) & 0x80000000u;
-              q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
+              // the code itself is the signed 2-bit field at bits 3kj+1 .. 3kj+2 ({nz, neg}: 01 = +1,
+              // 11 = -1, 00 = 0): one v_bfe_i32, a convert and an fma (code * g is exact)
+              const int code = ((int)(sv[e] << (29 - 3 * kj))) >> 30;
+              q = __builtin_fmaf((float)code, gv[e], q);
             }
             q += __shfl_xor(q, 16);
             q += __shfl_xor(q, 32);

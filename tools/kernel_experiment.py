@@ -33,6 +33,8 @@ VARIANTS = {
     "fwd_nopro": ["CIMQ_EXP_FWD_NOPRO"],
     "fwd_nostage": ["CIMQ_EXP_FWD_NOSTAGE"],
     "fwd_nogather": ["CIMQ_EXP_FWD_NOGATHER"],
+    "prep_noact": ["CIMQ_EXP_PREP_NOACT"],
+    "prep_nowt": ["CIMQ_EXP_PREP_NOWT"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
