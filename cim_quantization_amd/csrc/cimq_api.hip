@@ -198,6 +198,9 @@ struct Plan3 {
 
 inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// activation-prep blocks (grid-stride over 4-element items)
+static int act_blocks() { return tune("ACT_BLOCKS", 8192); }
+
 Plan3 v3_plan(const Geo& g) {
   Plan3 p;
   memset(&p, 0, sizeof(p));
@@ -464,8 +467,9 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   CtxLayout L = ctx_layout(g);
   const int blk = 256;
   {
-    int grid = cdiv(g.Nin, blk);
-    if (grid > 8192) grid = 8192;
+    // one 4-element item per thread up to 8192 blocks (fewer, fatter blocks measured slower)
+    int grid = cdiv(g.Nin, 4 * blk);
+    if (grid > act_blocks()) grid = act_blocks();
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     hipLaunchKernelGGL(prep_act_kernel, dim3(grid), dim3(blk), 0, s, g, x, sa, signed_act,
                        ctx + L.xcode, ctx + L.xhat);
@@ -904,7 +908,7 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
     a.Cp = (g.C + 15) / 16 * 16;
     a.pp = params_of(g, c);
     a.scal = scal;
-    a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 256), 8192);
+    a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 4 * 256), act_blocks());
     a.nwf = g.T * g.KS * g.NBLK * 64;
     const Plan7 p7 = v7_plan(g);
     a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;                   // general grad_x operand

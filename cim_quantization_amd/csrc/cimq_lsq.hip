@@ -159,6 +159,12 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
   }
   const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwt, e4 = e3 + a.nwc, total = e4 + a.npp;
   for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
+#ifdef CIMQ_EXP_PREP_NOFRAG
+    if (t < e4) continue;
+#endif
+#ifdef CIMQ_EXP_PREP_NOPARAMS
+    if (t >= e4) continue;
+#endif
     if (t < e1) wfrag_item(g, ws, a.wfrag, t);
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);

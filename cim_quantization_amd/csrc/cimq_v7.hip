@@ -108,6 +108,11 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
   const int nsteps = (oh_hi - oh_lo + v.NRS) / v.NRS;
   const int CPP = g.C * 3;
   const int RE = SS * v.SWD + 2;  // ring entry: input columns -1 .. SS*SWD (local), + pad
+  // index math by shifts (SWD = min(16, Wo), a power of two) and ring rows by a multiply-shift
+  // modulo (exact for the < 4096 relative rows of a band)
+  const int lsw = v.lw < 4 ? v.lw : 4;
+  const int rinv = (65536 + v.RSLOT - 1) / v.RSLOT;
+  auto ring_row = [&](int x) { return x - ((x * rinv) >> 16) * v.RSLOT; };
   const int rrow = v.NSEG * CPP * RE;  // floats per ring row
   float* ring = reinterpret_cast<float*>(smem);
   float* cel = ring + (size_t)v.RSLOT * rrow;
@@ -139,8 +144,8 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
     const bool pv = oh <= oh_e;
     const int pimg = (oh << v.lw) + ow;
     const size_t m = (size_t)b * g.P + pimg;
-    const int seg = ow / v.SWD, col = ow - seg * v.SWD;
-    float* rr = ring + (size_t)((oh - oh_lo) % v.RSLOT) * rrow + seg * CPP * RE;
+    const int seg = ow >> lsw, col = ow & (v.SWD - 1);
+    float* rr = ring + (size_t)ring_row(oh - oh_lo) * rrow + seg * CPP * RE;
     float gv[OBX][4];
 #pragma unroll
     for (int ob = 0; ob < OBX; ++ob)
@@ -294,14 +299,14 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
         const int iw = t & (g.W - 1), rest = t >> v.lwin;  // power-of-two W (v7_plan)
         const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
         const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
-        const int sg = iw / (SS * v.SWD), cl = iw - sg * (SS * v.SWD);
+        const int sg = iw >> (lsw + SS - 1), cl = iw & (SS * v.SWD - 1);
         float a = 0.f;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
           const int oo2 = ih + 1 - kh;  // = SS * oh
           const int oo = oo2 / SS;
           if (oo2 >= 0 && oo * SS == oo2 && oo >= oh_lo && oo <= oh_e) {
-            const float* e = ring + (size_t)((oo - oh_lo) % v.RSLOT) * rrow + (c * 3 + kh) * RE;
+            const float* e = ring + (size_t)ring_row(oo - oh_lo) * rrow + (c * 3 + kh) * RE;
             a += e[sg * CPP * RE + cl + 1];
             if (cl == SS * v.SWD - 1 && sg + 1 < v.NSEG) a += e[(sg + 1) * CPP * RE];
             if (SS == 1 && cl == 0 && sg > 0) a += e[(sg - 1) * CPP * RE + v.SWD + 1];
