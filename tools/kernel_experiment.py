@@ -35,6 +35,8 @@ VARIANTS = {
     "fwd_nogather": ["CIMQ_EXP_FWD_NOGATHER"],
     "prep_noact": ["CIMQ_EXP_PREP_NOACT"],
     "prep_nowt": ["CIMQ_EXP_PREP_NOWT"],
+    "prep_nofrag": ["CIMQ_EXP_PREP_NOACT", "CIMQ_EXP_PREP_NOFRAG"],
+    "prep_noparams": ["CIMQ_EXP_PREP_NOACT", "CIMQ_EXP_PREP_NOPARAMS"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
