@@ -1515,17 +1515,16 @@ __global__ __launch_bounds__(256) void cim_galpha_v5_kernel(Geo g, const uint8_t
 // independent loads in flight.  Returns the sum in the threads of the first wave.
 __device__ inline float reduce_chunks(const float* __restrict__ slab, size_t chunk_stride, int nchunks,
                                       size_t idx, float* red) {
+  // 8 independent loads in flight per lane: the few reducer blocks are latency-bound
   const int sub = threadIdx.x >> 6, nsub = blockDim.x >> 6;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int c = sub;
-  for (; c + 3 * nsub < nchunks; c += 4 * nsub) {
-    a0 += slab[(size_t)c * chunk_stride + idx];
-    a1 += slab[(size_t)(c + nsub) * chunk_stride + idx];
-    a2 += slab[(size_t)(c + 2 * nsub) * chunk_stride + idx];
-    a3 += slab[(size_t)(c + 3 * nsub) * chunk_stride + idx];
+  for (; c + 7 * nsub < nchunks; c += 8 * nsub) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += slab[(size_t)(c + u * nsub) * chunk_stride + idx];
   }
-  for (; c < nchunks; c += nsub) a0 += slab[(size_t)c * chunk_stride + idx];
-  red[threadIdx.x] = (a0 + a1) + (a2 + a3);
+  for (; c < nchunks; c += nsub) a[0] += slab[(size_t)c * chunk_stride + idx];
+  red[threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   float v = 0.f;
   if (sub == 0)
