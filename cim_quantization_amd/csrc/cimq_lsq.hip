@@ -229,21 +229,17 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
       p_div = -grad_t1 * (t1 / sw);
     }
   }
-  __syncthreads();
-  red[threadIdx.x] = p_mul;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int t = 0; t < 64; ++t) s += red[t];
-    a.wpart[2 * blk] = s;
-  }
-  __syncthreads();
-  red[threadIdx.x] = p_div;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int t = 0; t < 64; ++t) s += red[t];
-    a.wpart[2 * blk + 1] = s;
+  // both partials live in the first wave only: a butterfly there, no block barriers
+  if (sub == 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      p_mul += __shfl_xor(p_mul, o);
+      p_div += __shfl_xor(p_div, o);
+    }
+    if (threadIdx.x == 0) {
+      a.wpart[2 * blk] = p_mul;
+      a.wpart[2 * blk + 1] = p_div;
+    }
   }
 }
 
