@@ -39,7 +39,7 @@ XBAR, ADC = 128, 1.5
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward runs bf16 x3
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
-TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r01_v12", "pmc_traffic.json"))
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r02", "pmc_traffic.json"))
 # rocprof symbol of each v7-path kernel id (the names pmc_traffic.json is keyed by)
 V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, 3, ", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
               "gw_v7": "cimq::cim_bwd_gw_v7_kernel<3, 3>"}
@@ -53,11 +53,13 @@ def macs_per_sample():
     return sum(out_hw(h, s) ** 2 * o * c * 9 for _, c, o, h, s, _ in RESNET20)
 
 
-def build(device, batch, seed=0):
+def build(device, batch, seed=0, data_seed=None):
+    """The 19 layers (weights from ``seed``: identical on every rank) and one synthetic batch
+    of activations / output grads per layer (from ``data_seed``: each rank its own shard)."""
     import cim_quantization_amd._modules as my_nn
     torch.manual_seed(seed)
     layers, xs, gs = [], [], []
-    gen = torch.Generator().manual_seed(seed + 1)
+    gen = torch.Generator().manual_seed(seed + 1 if data_seed is None else data_seed)
     for name, c, o, h, s, nb in RESNET20:
         m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
                                abitslice=1, xbar=XBAR, adcbits=ADC, signed_xbar=True, stochastic_quant=False)
@@ -82,6 +84,10 @@ class Trainer:
         self.layers, self.world = layers, world
         self.bucket = GradBucket([p for m in layers for p in m.parameters()])  # one all-reduce per step
         self.bucket.own(layers)  # the layers add their grads straight into the bucket
+        # DDP's construction-time broadcast; the step sizes are re-sent once more after the
+        # first (initialising) step -- cim_quantization_amd/dist.py, DESIGN.md section 5
+        self.bucket.broadcast_from(0, layers)
+        self.synced_init = False
         self.flat = self.bucket.flat
         decay = [p for m in layers for nm, p in m.named_parameters() if not nm.startswith("alpha")]
         no_decay = [p for m in layers for nm, p in m.named_parameters() if nm.startswith("alpha")]
@@ -102,7 +108,15 @@ class Trainer:
 
     def step(self, xs, gs):
         self.compute(xs, gs)
+        if not self.synced_init:
+            self.bucket.broadcast_from(0, self.layers)  # rank 0's initialised alpha_* / signed_act
+            self.synced_init = True
         self.finish()
+
+    def forward_only(self, xs):
+        with torch.no_grad():
+            for m, x in zip(self.layers, xs):
+                m(x)
 
     def capture(self, xs, gs):
         """Record fwd+bwd of all layers as one HIP graph: a step is then one graph launch plus the
@@ -121,6 +135,16 @@ class Trainer:
         self.graph.replay()
         self.finish()
 
+    def capture_forward(self, xs):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self.forward_only(xs)
+        torch.cuda.current_stream().wait_stream(side)
+        self.fgraph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.fgraph):
+            self.forward_only(xs)
+
 
 def timed(trainer, xs, gs, steps, dev, world, graph):
     if world > 1:
@@ -136,6 +160,53 @@ def timed(trainer, xs, gs, steps, dev, world, graph):
     if world > 1:
         dist.barrier()
     return time.perf_counter() - t0
+
+
+def timed_forward(trainer, xs, steps, dev, world, graph):
+    """The metric's own quantized-MAC/s (logical MAC / forward time): the
+    forward of the 19 convs only, bracketed like the step timing."""
+    if graph:
+        trainer.capture_forward(xs)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if graph:
+            trainer.fgraph.replay()
+        else:
+            trainer.forward_only(xs)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def source_sha():
+    """sha256 of the kernel sources: ties a committed PMC traffic file to the kernels it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(REPO, "cim_quantization_amd", "csrc", "*")))
+    for f in files + [os.path.join(REPO, "include", "cimq.h")]:
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(dominant):
+    """Launch-weighted HBM bytes per launch of the dominant kernel family from the committed
+    PMC passes (tools/pmc_traffic.py), or (None, reason) when they measured other sources."""
+    if not os.path.exists(TRAFFIC_JSON):
+        return None, "no PMC traffic file"
+    tj = json.load(open(TRAFFIC_JSON))
+    meta = tj.pop("_meta", {})
+    if meta.get("source_sha") != source_sha():
+        return None, f"{os.path.relpath(TRAFFIC_JSON, REPO)} measured other kernel sources"
+    hits = [(v["traffic_bytes"], v.get("dispatches", 1)) for k, v in tj.items() if k.startswith(V7_SYMBOLS[dominant])]
+    if not hits:
+        return None, "dominant kernel absent from the PMC file"
+    n = sum(c for _, c in hits)
+    return sum(b * c for b, c in hits) / n, os.path.relpath(TRAFFIC_JSON, REPO)
 
 
 def layer_breakdown(trainer, xs, gs, dev):
@@ -208,7 +279,7 @@ def main():
     from cim_quantization_amd import _lib
     _lib.load()  # fail loudly if the HIP library is missing
 
-    layers, xs, gs = build(dev, args.batch, seed=1234 + rank)
+    layers, xs, gs = build(dev, args.batch, seed=1234, data_seed=1235 + 1000 * rank)
     tr = Trainer(layers, world)
     for _ in range(max(1, args.warmup)):  # the first step runs the LSQ / alpha_cim init (lsq.py:532-563)
         tr.step(xs, gs)
@@ -237,10 +308,11 @@ def main():
     else:
         with _lib.KernelTimer(dominant, max_launches=len(RESNET20) * args.steps + 8) as kt:
             elapsed = timed(tr, xs, gs, args.steps, dev, world, False)
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    fwd_elapsed = timed_forward(tr, xs, args.steps, dev, world, graph)
+    t = torch.tensor([elapsed, fwd_elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = t.item()
+    elapsed, fwd_elapsed = t.tolist()
     breakdown = layer_breakdown(tr, xs, gs, dev)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -256,13 +328,7 @@ def main():
     mfma_ops = flops_l * (9.0 if dominant == "fwd_v7" else 3.0)
     mfma_peak = PEAK_I8_TOPS if dominant == "fwd_v7" else PEAK_BF16_TFLOPS
     t_mfma = mfma_ops / (mfma_peak * 1e12)
-    traffic = None
-    if os.path.exists(TRAFFIC_JSON):
-        import json as _json
-        tj = _json.load(open(TRAFFIC_JSON))
-        hits = [v["traffic_bytes"] for k, v in tj.items() if k.startswith(V7_SYMBOLS[dominant])]
-        if hits:
-            traffic = sum(hits) / len(hits)
+    traffic, traffic_source = measured_traffic(dominant)
     if t_hbm >= t_mfma:
         roof = {"bound": "hbm", "achieved": bytes_l / (avg_launch_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                 "unit": "GB/s"}
@@ -280,6 +346,10 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "ms_per_layer_fwd_bwd": ms_per_step / len(RESNET20),
+        "value_semantics": "logical MAC (B*P*O*K, flops_counter.py:314-318) of the 19 convs per fwd+bwd+SGD "
+                           "step / step time; the forward-only rate SURVEY 8(d) defines is fwd_only.value",
+        "fwd_only": {"value": macs_step / (fwd_elapsed / args.steps), "unit": "MAC/s",
+                     "ms_per_forward": fwd_elapsed / args.steps * 1e3},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -293,7 +363,7 @@ def main():
                          avg_launch_us=avg_launch_ms * 1e3, launches=kt.launches,
                          algo_bytes_per_launch=bytes_l, algo_flops_per_launch=flops_l,
                          t_hbm_us=t_hbm * 1e6, t_mfma_us=t_mfma * 1e6,
-                         traffic_source=os.path.relpath(TRAFFIC_JSON, REPO) if traffic is not None else None),
+                         traffic_source=traffic_source),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
     }

@@ -18,6 +18,10 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcimq.so")
 ARCH = os.environ.get("CIMQ_OFFLOAD_ARCH", "gfx950")
+# the kernels are written for 64-lane waves (wave-id = threadIdx >> 6, 32..1 shuffle
+# butterflies); gfx9 targets (CDNA) have no wave32 mode, so anything else is refused
+if not ARCH.startswith("gfx9"):
+    raise SystemExit(f"libcimq targets wave64 CDNA GPUs (gfx9xx); CIMQ_OFFLOAD_ARCH={ARCH!r} refused")
 
 
 def sources():

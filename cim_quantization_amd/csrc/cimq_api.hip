@@ -40,13 +40,18 @@ int check_hip(const char* where) {
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-// tuning knobs for experiments (tools/): CIMQ_TUNE_<name>=<int> overrides a launch shape
+// tuning knobs for experiments (tools/, built with -DCIMQ_TUNING): CIMQ_TUNE_<name>=<int>
+// overrides a launch shape; the shipped library compiles them to the defaults
+#ifdef CIMQ_TUNING
 int tune(const char* name, int dflt) {
   char key[64];
   snprintf(key, sizeof(key), "CIMQ_TUNE_%s", name);
   const char* v = getenv(key);
   return v ? atoi(v) : dflt;
 }
+#else
+constexpr int tune(const char*, int dflt) { return dflt; }
+#endif
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 int make_geo(const cimq_conv_desc* d, Geo* out) {
@@ -267,7 +272,7 @@ Plan3 v3_plan(const Geo& g) {
   }
   const size_t pg = a16((size_t)v.NCG * v.RH * v.WP * g.NBP);
   const size_t gw_tail = (size_t)g.KS * 64 * 4 + (size_t)g.nbw * nog * g.KS * 1024 + (size_t)nkj * nog * 16 * 16 +
-                         a16((size_t)nkj * 32 * 4) + ckl;
+                         a16((size_t)nkj * 32 * 4 * 4) + ckl;  // init: per-wave |u| rows
   p.lds_gw = std::max(a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + 128 * 4 +
              a16((size_t)nkj * 16 * 4) + ckl;
   p.lds_init = pg + gw_tail;
@@ -587,14 +592,20 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
                        reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
     prof_end(slot, s);
     return check_hip("cim_bwd_gw_v5");
-  } else if (p.ok) {
-    const size_t lds = p.lds_init;
-    auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, INIT> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, INIT>;
-    CIMQ_TRY(set_lds(kern, lds));
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
-                       reinterpret_cast<const v4i*>(ctx + L.wfrag), pp, sw, sa, gout, W.rows,
-                       reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
-  } else {
+  }
+  if constexpr (INIT) {
+    // alpha_cim init sums (the v3 kernel runs only in this mode)
+    if (p.ok && p.lds_init <= kLdsMax - 512) {
+      const size_t lds = p.lds_init;
+      auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, true> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, true>;
+      CIMQ_TRY(set_lds(kern, lds));
+      hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
+                         reinterpret_cast<const v4i*>(ctx + L.wfrag), pp, sw, sa, gout, W.rows,
+                         reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
+      return check_hip("cim_bwd_gw_v3(init)");
+    }
+  }
+  {
     const size_t lds = lds_gw(g);
     auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;
     CIMQ_TRY(set_lds(kern, lds));

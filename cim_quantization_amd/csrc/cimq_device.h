@@ -6,6 +6,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+// The kernels assume 64-lane waves (shuffle butterflies over 32..1, threadIdx >> 6 as the
+// wave id): build.py accepts only gfx9 (wave64-only) targets.
 namespace cimq {
 
 typedef int v4i __attribute__((ext_vector_type(4)));

@@ -885,7 +885,10 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const int tlen = g.KS * 64;
   const int nkj = g.nbw * g.nba;
   const int ncol = 32;
-  float* qacc = reinterpret_cast<float*>(smem + off);   // [nkj][32]: sum code*g (|u| in INIT)
+  // [nkj][32]: sum code*g; INIT: [4 waves][nkj][32] sums of |u|, one writer per slot and
+  // added in wave order at the end (bit-reproducible alpha_cim init); the extra rows
+  // overlap gwacc / Xb, which INIT does not use (lds_gw leaves room: nba*KS*4096 >= 384*nkj)
+  float* qacc = reinterpret_cast<float*>(smem + off);
   off += sizeof(float) * nkj * ncol;
   float* gwacc = reinterpret_cast<float*>(smem + off);  // [FBT*16][32]
   off += sizeof(float) * g.FBT * 16 * ncol;
@@ -903,8 +906,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const bool ternary_fast = (!literal) && g.mode == ADC_TERNARY;
   const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
 
-  for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) qacc[t] = 0.f;
-  for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
+  for (int t = threadIdx.x; t < nkj * ncol * (INIT ? 4 : 1); t += blockDim.x) qacc[t] = 0.f;
+  if (!INIT)
+    for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
   v4f gwa[FBMAX][2];
 #pragma unroll
   for (int a = 0; a < FBMAX; ++a) { gwa[a][0] = v4f{0, 0, 0, 0}; gwa[a][1] = v4f{0, 0, 0, 0}; }
@@ -1008,7 +1012,11 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
               // lanes l, l^16, l^32, l^48 share the column: fold the 16 pixel rows, then LDS
               qs += __shfl_xor(qs, 16);
               qs += __shfl_xor(qs, 32);
-              if (g4 == 0 && (INIT || has_code)) atomicAdd(&qacc[kj * ncol + ocol], qs);
+              if (INIT) {
+                if (g4 == 0) qacc[(wave * nkj + kj) * ncol + ocol] += qs;
+              } else if (g4 == 0 && has_code) {
+                atomicAdd(&qacc[kj * ncol + ocol], qs);
+              }
             }
           }
         }
@@ -1082,7 +1090,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
     const int o = og * 32 + col;
     if (o < g.Opad) {
       const int k = q / g.nba, j = q - k * g.nba;
-      ga_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qacc[t];
+      float qv = qacc[t];
+      if (INIT) qv = ((qv + qacc[nkj * ncol + t]) + qacc[2 * nkj * ncol + t]) + qacc[3 * nkj * ncol + t];
+      ga_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qv;
     }
   }
   if (INIT) return;
@@ -1090,61 +1100,6 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
     const int fl = t / ncol, col = t - fl * ncol;
     const int o = og * 32 + col;
     if (o < g.Opad) gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o] = gwacc[t];
-  }
-}
-
-
-// grad_w[o, f] = (sa/nbw) * sum_chunks slab ;  grad_alpha = c * mask * sum_chunks
-__global__ void reduce_gw_kernel(Geo g, int nchunks, const float* __restrict__ gw_slab,
-                                 const float* __restrict__ sa_p, float* __restrict__ grad_w) {
-  const float scale = (*sa_p) / (float)g.nbw;
-  const int total = g.O * g.K;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int o = t / g.K, f = t - o * g.K;
-    const int i = f / g.xbar, fl = f - i * g.xbar;
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c) s += gw_slab[(((size_t)c * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o];
-    grad_w[t] = s * scale;
-  }
-}
-
-__global__ void reduce_galpha_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab, Params pp,
-                                     float cgrad, float* __restrict__ grad_alpha) {
-  const int nkj = g.nbw * g.nba;
-  const int total = g.T * nkj * g.O;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    // output layout [1, T, nbw, nba, 1, O]
-    int r = t;
-    const int o = r % g.O; r /= g.O;
-    const int j = r % g.nba; r /= g.nba;
-    const int k = r % g.nbw;
-    const int i = r / g.nbw;
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c)
-      s += ga_slab[(((size_t)c * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o];
-    grad_alpha[t] = (cgrad * pp.ckj[k * g.nba + j]) * s;
-  }
-}
-
-// alpha_init = 2*mean|u|/sqrt(Qp_adc); zeros -> sw*sa   (lsq.py:560-562)
-__global__ void reduce_alpha_init_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab,
-                                         const float* __restrict__ sw_p, const float* __restrict__ sa_p,
-                                         float count, float sqrt_qp, float* __restrict__ alpha_init) {
-  const int nkj = g.nbw * g.nba;
-  const int total = g.T * nkj * g.O;
-  const float fill = (1.0f * (*sw_p)) * (*sa_p);
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    int r = t;
-    const int o = r % g.O; r /= g.O;
-    const int j = r % g.nba; r /= g.nba;
-    const int k = r % g.nbw;
-    const int i = r / g.nbw;
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c)
-      s += ga_slab[(((size_t)c * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o];
-    const float mean = s / count;
-    float v = (2.0f * mean) / sqrt_qp;
-    alpha_init[t] = (v == 0.f) ? fill : v;
   }
 }
 

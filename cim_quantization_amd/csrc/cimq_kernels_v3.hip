@@ -1014,7 +1014,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
   int* ptab = reinterpret_cast<int*>(cur); cur += KS * 64 * 4;
   v4i* wfl = reinterpret_cast<v4i*>(cur); cur += (size_t)g.nbw * NOB * KS * 1024;     // [k][ob][ks][64]
   int4* prm = reinterpret_cast<int4*>(cur); cur += (size_t)nkj * NOB * 16 * 16;       // [j][k][NOB*16]
-  float* qacc = reinterpret_cast<float*>(cur); cur += al16((size_t)nkj * 32 * 4);
+  // INIT: one |u| partial-sum row per wave, summed in wave order at the end (no float
+  // atomics: the alpha_cim init is bit-reproducible, lsq.py:559-562)
+  float* qacc = reinterpret_cast<float*>(cur); cur += al16((size_t)nkj * 32 * 4 * (INIT ? 4 : 1));
   float* ckl = reinterpret_cast<float*>(cur);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1026,7 +1028,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
   const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
   const int Wo = 1 << v.lw;
 
-  for (int t = threadIdx.x; t < nkj * 32; t += blockDim.x) qacc[t] = 0.f;
+  for (int t = threadIdx.x; t < nkj * 32 * (INIT ? 4 : 1); t += blockDim.x) qacc[t] = 0.f;
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
   build_ptab(g, i, KS, v.RH, v.WP, ptab, c0);
   batched_copy<4>(g.nbw * NOB * KS * 64, wfl, [&](int idx) -> v4i {
@@ -1159,7 +1161,11 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
               if (INIT || has_code) {
                 qs += __shfl_xor(qs, 16);
                 qs += __shfl_xor(qs, 32);
-                if (g4 == 0) atomicAdd(&qacc[kj * 32 + ocol], qs);
+                if (INIT) {
+                  if (g4 == 0) qacc[(wave * nkj + kj) * 32 + ocol] += qs;  // one writer per slot
+                } else if (g4 == 0) {
+                  atomicAdd(&qacc[kj * 32 + ocol], qs);
+                }
               }
 #endif
             }
@@ -1232,7 +1238,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
   for (int t = threadIdx.x; t < nkj * 32; t += blockDim.x) {
     const int q = t >> 5, col = t & 31;
     const int o = og * 32 + col;
-    if (o < g.Opad) ga_slab[(((size_t)mc * g.T + i) * nkj + q) * g.Opad + o] = qacc[t];
+    float qv = qacc[t];
+    if (INIT) qv = ((qv + qacc[nkj * 32 + t]) + qacc[2 * nkj * 32 + t]) + qacc[3 * nkj * 32 + t];
+    if (o < g.Opad) ga_slab[(((size_t)mc * g.T + i) * nkj + q) * g.Opad + o] = qv;
   }
   if (INIT) return;
   for (int t = threadIdx.x; t < g.FBT * 16 * 32; t += blockDim.x) {
@@ -1451,60 +1459,6 @@ __global__ __launch_bounds__(256, 1) void cim_bwd_gw_v5_kernel(Geo g, V3 v, cons
     const int fl = t >> 4, col = t & 15;
     const int oo = ob * 16 + col;
     gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + oo] = gwacc[t];
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// grad_alpha_cim partial sums from the state words: ga[i, k, j, o] = sum_m code_ijk[m, o] *
-// g[m, o] (lsq.py:321-333).  Block = (pixel chunk, (i, k)); thread = one channel o (O | 256)
-// and a strided run of 4-pixel quads; per-(o, j) sums meet in LDS once.
-// ---------------------------------------------------------------------------------------
-template <int NBP>
-__global__ __launch_bounds__(256) void cim_galpha_v5_kernel(Geo g, const uint8_t* __restrict__ st,
-                                                            const float* __restrict__ gout, int rows_per_chunk,
-                                                            float* __restrict__ ga_slab) {
-  typedef typename StWord<NBP>::T SW;
-  __shared__ float red[256 * 8];
-  const int ik = blockIdx.y, i = ik / g.nbw, k = ik - i * g.nbw;
-  const int nkj = g.nbw * g.nba;
-  const int o = threadIdx.x % g.O, qs0 = threadIdx.x / g.O, qstep = blockDim.x / g.O;
-  const size_t MQ = (size_t)g.M >> 2;
-  const int mb = (int)blockIdx.x * rows_per_chunk;
-  const int q0 = mb >> 2, q1 = min(mb + rows_per_chunk, g.M) >> 2;
-  float acc[NBP];
-#pragma unroll
-  for (int j = 0; j < NBP; ++j) acc[j] = 0.f;
-  for (int q = q0 + qs0; q < q1; q += qstep) {
-    const size_t e = ((size_t)ik * MQ + q) * g.O + o;
-    SW sv[4];
-    if (sizeof(SW) == 2) {
-      const uint2 w = reinterpret_cast<const uint2*>(st)[e];
-      sv[0] = (SW)w.x; sv[1] = (SW)(w.x >> 16); sv[2] = (SW)w.y; sv[3] = (SW)(w.y >> 16);
-    } else {
-      const uint4 w = reinterpret_cast<const uint4*>(st)[e];
-      sv[0] = w.x; sv[1] = w.y; sv[2] = w.z; sv[3] = w.w;
-    }
-    const float4 g4v = load_g4(g, gout, (size_t)q * 4, o);
-    const float gq[4] = {g4v.x, g4v.y, g4v.z, g4v.w};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float gv = gq[r];
-#pragma unroll
-      for (int j = 0; j < NBP; ++j) {
-        const uint32_t bits = sv[r] >> (3 * j);
-        const float c = (bits & 2u) ? ((bits & 4u) ? -gv : gv) : 0.f;
-        acc[j] += c;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NBP; ++j) red[j * 256 + threadIdx.x] = acc[j];
-  __syncthreads();
-  for (int t = threadIdx.x; t < g.O * g.nba; t += blockDim.x) {
-    const int j = t / g.O, oo = t - j * g.O;
-    float sacc = 0.f;
-    for (int s2 = 0; s2 < qstep; ++s2) sacc += red[j * 256 + s2 * g.O + oo];
-    ga_slab[(((size_t)blockIdx.x * g.T + i) * nkj + k * g.nba + j) * g.Opad + oo] = sacc;
   }
 }
 

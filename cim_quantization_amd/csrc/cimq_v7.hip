@@ -5,17 +5,16 @@
 // ADC code (lsq.py:321-332) of that partial sum, 3 bits at 3*(k*nba + j).  Two kernels
 // consume them:
 //
-//  * cim_bwd_gx_v7_kernel -- grad_x as the UNFOLDED product, then the nn.Fold adjoint in LDS:
+//  * cim_bwd_gx_v8_kernel -- grad_x as the UNFOLDED product, folded without atomics:
 //      gx_unf[m, f] = sum_kappa W_i[f, kappa] * G_i[m, kappa],  kappa = (k, o),
 //      G_i[m, (k, o)] = g[m, o] * sum_j cE_kj * pass_ijk[m, o]       (cE = mask * 2^-bsa*j)
 //    on v_mfma_f32_16x16x32_bf16 with G split hi/mid/lo (fp32-exact products: W is a small
 //    integer).  The lane that reads the state words of pixel m (its MFMA column) for four
 //    consecutive channels IS the B-operand lane of (m, 8 kappa) -- G is built in registers,
-//    never staged.  Each 16 x 16 (f, m) result tile is added into an LDS image of the block's
-//    band of input rows (ds_add_f32: 16 consecutive columns x 4 kernel taps per
-//    instruction); the fused LSQ activation backward (lsq.py:549) reads the finished image.
-//    Only f-blocks that hold tile i's rows are multiplied (no tile-padding waste).
-//
+//    never staged.  The rows f are ordered (c, kh, kw), so the nn.Fold adjoint along kw is
+//    three DPP lane shifts in registers, and along kh a pass over an LDS ring of output rows
+//    in which every value is written by exactly one lane; that pass also applies the fused
+//    LSQ activation backward (lsq.py:549).
 //  * cim_bwd_gw_v7_kernel -- grad_w (+ grad_alpha_cim partials) as a weight-gradient conv:
 //      gw[(c, kh, kw), o] = sum_j sum_m xhat_j[c, ih(m, kh), iw(m, kw)] * g[m, o] * D_ij[m, o]
 //    with D_ij = sum_k cD_kj * pass_ijk, i = tile of (c, kh, kw).  K = 32 output pixels per
@@ -343,167 +342,6 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
       for (int w = 0; w < 4 * NPART; ++w) t += red[w];
       gsa_part[blockIdx.x] = t;
     }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// grad_x, v7 (kept for reference / experiments): LDS float-atomic fold
-// ---------------------------------------------------------------------------------------
-template <int NBW, int OBX, bool LSQ>
-__global__ __launch_bounds__(256, 2) void cim_bwd_gx_v7_kernel(Geo g, V7 v, const uint32_t* __restrict__ st,
-                                                            const v4i* __restrict__ wgx, Params pp,
-                                                            const float* __restrict__ sw_p,
-                                                            const float* __restrict__ sa_p,
-                                                            const float* __restrict__ gout,
-                                                            const float* __restrict__ x, float* __restrict__ gx,
-                                                            float* __restrict__ gsa_part) {
-  constexpr int NKS = (NBW * OBX + 1) / 2;  // 32-wide kappa chunks
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int nkj = NBW * g.nba;
-  const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
-  const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB), nrow = r1 - r0;
-  int oh_lo = r0 + g.PH - (g.KH - 1);
-  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.SH - 1) / g.SH;
-  const int oh_hi = min(g.Ho - 1, (r1 - 1 + g.PH) / g.SH);
-  const int npb = (oh_hi - oh_lo + 1) << v.lw;
-  const int ngrp = (npb + 15) >> 4;
-  const int RW = v.RB * g.W;
-
-  uint8_t* cur = smem;
-  float* gacc = reinterpret_cast<float*>(cur); cur += al16((size_t)g.C * RW * 4);
-  v4i* wfr = reinterpret_cast<v4i*>(cur); cur += (size_t)v.FBX * NKS * 64 * 16;
-  int* ftab = reinterpret_cast<int*>(cur); cur += (size_t)v.FBX * 16 * 4;
-  float* cel = reinterpret_cast<float*>(cur); cur += 64 * 4;
-  float* red = reinterpret_cast<float*>(cur);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const float sw = *sw_p, sa = *sa_p;
-  const int Wo = 1 << v.lw;
-
-  for (int t = threadIdx.x; t < g.C * RW; t += blockDim.x) gacc[t] = 0.f;
-  for (int t = threadIdx.x; t < nkj; t += blockDim.x) cel[t] = pp.ckj[nkj + t];
-
-  for (int i = 0; i < g.T; ++i) {
-    const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;
-    __syncthreads();
-    {
-      const v4i* src = wgx + (size_t)i * v.FBX * NKS * 64;
-      for (int t = threadIdx.x; t < fbn * NKS * 64; t += blockDim.x) wfr[t] = src[t];
-      for (int t = threadIdx.x; t < fbn * 16; t += blockDim.x) {
-        const int f = i * g.xbar + t;
-        int code = -1;
-        if (t < g.xbar && f < g.K) {
-          const int c = f / g.KHW, rem = f - c * g.KHW;
-          const int kh = rem / g.KW, kw = rem - kh * g.KW;
-          code = (c * RW) | (kh << 20) | (kw << 25);
-        }
-        ftab[t] = code;
-      }
-    }
-    __syncthreads();
-    for (int grp = wave; grp < ngrp; grp += 4) {
-      const int p = (grp << 4) + r16;  // band-relative output pixel = this lane's MFMA column
-      const bool pv = p < npb;
-      const int oh = oh_lo + (p >> v.lw), ow = p & (Wo - 1);
-      const int pimg = (oh << v.lw) + ow;
-      const size_t m = (size_t)b * g.P + pimg;
-      uint32_t sv[OBX][4];
-      float gv[OBX][4];
-#pragma unroll
-      for (int ob = 0; ob < OBX; ++ob) {
-        const int o0 = ob * 16 + 4 * g4;
-        if (pv) {
-          const uint4 s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + o0);
-          sv[ob][0] = s4.x; sv[ob][1] = s4.y; sv[ob][2] = s4.z; sv[ob][3] = s4.w;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            gv[ob][r] = g.onchw ? gout[((size_t)b * g.O + o0 + r) * g.P + pimg] : gout[m * g.O + o0 + r];
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) { sv[ob][r] = 0u; gv[ob][r] = 0.f; }
-        }
-      }
-      v4f acc[8];
-#pragma unroll
-      for (int fb = 0; fb < 8; ++fb) acc[fb] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        float G[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int kb = 2 * s + (e >> 2), r = e & 3;
-          G[e] = 0.f;
-          if (kb < NBW * OBX) {
-            const int k = kb / OBX, ob = kb - k * OBX;
-            float E = 0.f;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (j < g.nba) E += ((sv[ob][r] >> (3 * (k * g.nba + j))) & 1u) ? cel[k * g.nba + j] : 0.f;
-            G[e] = gv[ob][r] * E;
-          }
-        }
-        v8bf bh, bm, bl;
-        split3x8(G, bh, bm, bl);
-#pragma unroll
-        for (int fb = 0; fb < 8; ++fb) {
-          if (fb < fbn) {
-            const v8bf a = as_v8bf(wfr[(fb * NKS + s) * 64 + lane]);
-            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
-            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
-            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
-          }
-        }
-      }
-      // nn.Fold adjoint: acc[fb][r] = gx_unf[f = fb*16 + 4*g4 + r][this lane's pixel]
-      if (pv) {
-        const int ihb = oh * g.SH - g.PH - r0, iwb = ow * g.SW - g.PW;
-#pragma unroll
-        for (int fb = 0; fb < 8; ++fb) {
-          if (fb < fbn) {
-            const int4 c4 = reinterpret_cast<const int4*>(ftab)[fb * 4 + g4];
-            const int cs[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int code = cs[r];
-              const int ih = ihb + ((code >> 20) & 31), iw = iwb + ((code >> 25) & 31);
-              if (code >= 0 && (unsigned)ih < (unsigned)nrow && (unsigned)iw < (unsigned)g.W)
-                atomicAdd(&gacc[(code & 0xFFFFF) + ih * g.W + iw], acc[fb][r]);
-            }
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // epilogue: scale, fused LSQ activation backward (as cim_bwd_gx_v6_kernel), one store
-  const float scale = sw / (float)g.nba;
-  float part = 0.f;
-  const int nown = g.C * nrow * g.W;
-  for (int t = threadIdx.x; t < nown; t += blockDim.x) {
-    const int c = t / (nrow * g.W), q = t - c * (nrow * g.W);
-    const size_t gi = (((size_t)b * g.C + c) * g.H + r0) * g.W + q;
-    const float gqv = gacc[c * RW + q] * scale;
-    if (LSQ) {
-      const float xv = x[gi];
-      const float y1 = xv / sa;
-      const float cl = clamp_nan(y1, 0.f, g.lsq_qp);
-      const float rr2 = rintf(cl);
-      const float rp = (rr2 - cl) + cl;
-      const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
-      const float gy = pass ? gqv * sa : 0.f;
-      gx[gi] = gy / sa;
-      part += gqv * rp;
-      part += -(gy * (y1 / sa));
-    } else {
-      gx[gi] = gqv;
-    }
-  }
-  if (LSQ) {
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) red[wave] = part;
-    __syncthreads();
-    if (threadIdx.x == 0) gsa_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
   }
 }
 

@@ -1,16 +1,43 @@
-"""Data-parallel gradient exchange for the CiM layers.
+"""Data-parallel training state for the CiM layers.
 
 Samples are independent through the CiM conv, so the path shards by batch: one process per
-GPU, and one all-reduce per step of every gradient.  The gradients of all parameters live
-in ONE flat fp32 bucket (1.17 MB for ResNet-20): autograd accumulates straight into it
-(each ``p.grad`` is a view), and the exchange is a single ``all_reduce`` + scale, which on
-ROCm runs on RCCL over xGMI (backend ``"nccl"``).  Gradients keep the reference's
-local-batch semantics (its DDP run averages per-GPU gradients the same way).
+GPU, one all-reduce per step of every gradient.  The gradients of all parameters live in ONE
+flat fp32 bucket (1.17 MB for ResNet-20): autograd accumulates straight into it (each
+``p.grad`` is a view), and the exchange is a single ``all_reduce`` + scale, which on ROCm
+runs on RCCL over xGMI (backend ``"nccl"``).  Gradients keep the reference's local-batch
+semantics (its DDP run averages per-GPU gradients the same way: ``ga``, the grad_scale
+factors and ``ps.numel()`` of lsq.py:323,547,553 see the local batch).
+
+What the reference's DDP wrapper does besides the all-reduce (examples/__init__.py:693-731),
+and how this module covers it:
+
+* construction-time broadcast of rank 0's parameters and buffers -> ``broadcast_from(0)``;
+* the first training step initialises ``alpha_act`` / ``alpha_weight`` / ``alpha_cim`` and
+  ``signed_act`` from each rank's OWN batch (lsq.py:532-563), after DDP's broadcast, so the
+  reference's ranks keep different step sizes for the whole run.  Decision (DESIGN.md section
+  5): call ``broadcast_from(0)`` again right after that first step's backward, before the
+  optimizer step -- every rank then continues from rank 0's initialised step sizes and the
+  replicas stay identical.  The first step's own gradients are the local ones, as in the
+  reference.
+* DDP's per-forward buffer broadcast only re-sends ``init_state`` / ``signed_act`` /
+  ``init_state_cim``, which the post-init broadcast already made identical.
+
+Callers zero the bucket with ``zero()``.  ``optimizer.zero_grad()`` (set_to_none=True since
+torch 2.0) detaches ``p.grad`` from the bucket; ``exchange()`` detects that (by data pointer)
+and copies such gradients back into their slot before reducing, so a misused bucket costs a
+copy but never silently exchanges stale values.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+
+def _world(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
 
 
 class GradBucket:
@@ -21,11 +48,18 @@ class GradBucket:
         n = sum(p.numel() for p in self.params)
         dev = device if device is not None else self.params[0].device
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.views = []
         off = 0
         for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
             off += p.numel()
         self.nbytes = n * 4
+        self.reattached = 0  # gradients found detached from the bucket (diagnostic)
+        self._attach()
+
+    def _attach(self):
+        for p, v in zip(self.params, self.views):
+            p.grad = v
 
     def own(self, modules):
         """Let the CiM layers among ``modules`` add their parameter gradients into this bucket
@@ -38,13 +72,52 @@ class GradBucket:
                     m.accumulate_grads_in_place = True
         return self
 
+    def sync_views(self):
+        """Make every ``p.grad`` the bucket view again, copying gradients that autograd put in
+        fresh tensors (after ``zero_grad(set_to_none=True)`` or a reassigned ``.grad``)."""
+        for p, v in zip(self.params, self.views):
+            g = p.grad
+            if g is not None and g.data_ptr() == v.data_ptr() and g.shape == v.shape:
+                continue
+            self.reattached += 1
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g.detach().reshape(v.shape))
+            p.grad = v
+
     def exchange(self, group=None):
         """Average the bucket over the ranks of ``group`` (no-op for a single process)."""
-        if dist.is_available() and dist.is_initialized():
-            world = dist.get_world_size(group)
-            if world > 1:
-                dist.all_reduce(self.flat, group=group)
-                self.flat.mul_(1.0 / world)
+        self.sync_views()
+        world = _world(group)
+        if world > 1:
+            dist.all_reduce(self.flat, group=group)
+            self.flat.mul_(1.0 / world)
 
     def zero(self):
         self.flat.zero_()
+        self._attach()
+
+    def broadcast_from(self, src=0, modules=(), group=None):
+        """Copy rank ``src``'s parameters (and the buffers of ``modules``) to every rank: the
+        DDP construction-time broadcast, and the post-initialisation re-sync of the
+        data-dependent step sizes (module docstring).  One coalesced collective per dtype."""
+        if _world(group) <= 1:
+            return
+        seen, tensors = set(), []
+        for t in list(self.params) + [b for m in modules for b in m.buffers()]:
+            if id(t) not in seen:
+                seen.add(id(t))
+                tensors.append(t)
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault((t.dtype, t.device), []).append(t)
+        with torch.no_grad():
+            for ts in by_dtype.values():
+                flat = _flatten_dense_tensors([t.detach() for t in ts])
+                dist.broadcast(flat, src, group=group)
+                for t, v in zip(ts, _unflatten_dense_tensors(flat, ts)):
+                    t.copy_(v)
+        for m in modules:
+            if hasattr(m, "_state_cache"):
+                m._state_cache = None  # init flags may have changed with the buffers

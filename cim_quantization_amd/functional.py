@@ -81,12 +81,14 @@ class get_cim_output_signed(torch.autograd.Function):
                                     out.data_ptr(), cbuf.data_ptr(), None, _stream()), "cimq_forward")
         ctx.desc, ctx.sizes = desc, sizes
         ctx.bufs = (xq, sa, sw, al, bm, sg, cbuf)
+        ctx.save_for_backward(x, w)  # autograd's version check: in-place edits before backward raise
         ctx.wshape, ctx.xshape = wq.shape, xq.shape
         ctx.has_alpha = alpha_cim is not None
         return out
 
     @staticmethod
     def backward(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018 -- raises if x / w changed in place since the forward
         xq, sa, sw, al, bm, sg, cbuf = ctx.bufs
         dev = xq.device
         g = grad_output.detach().to(torch.float32).contiguous()
@@ -133,12 +135,14 @@ class _CimConv2dLSQ(torch.autograd.Function):
                                     out.data_ptr(), cbuf.data_ptr(), None, _stream()), "cimq_forward")
         ctx.desc, ctx.sizes = desc, sizes
         ctx.bufs = (xc, sa_, sw_, al, bm, sg, cbuf)
+        ctx.save_for_backward(x, w_q)
         ctx.wshape = wq.shape
         ctx.has_alpha = alpha_q is not None
         return out
 
     @staticmethod
     def backward(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018 -- version check of x / w_q
         xc, sa, sw, al, bm, sg, cbuf = ctx.bufs
         dev = xc.device
         g = grad_output.detach().to(torch.float32).contiguous()
@@ -209,6 +213,9 @@ class _CimModuleConv(torch.autograd.Function):
                    "cimq_module_forward")
         ctx.desc, ctx.lsq, ctx.sizes = desc, lsq, sizes
         ctx.bufs = (xc, wc, aa, aw, ac, bm, sg, cbuf)
+        # the backward reads x and the raw parameters again (act-LSQ / weight-LSQ STE); saving
+        # them lets autograd's version counters catch an in-place change in between
+        ctx.save_for_backward(x, weight, alpha_act, alpha_weight, alpha_cim)
         ctx.params = (weight, alpha_act, alpha_weight, alpha_cim) if accumulate else None
         return out
 
@@ -231,6 +238,7 @@ class _CimModuleConv(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018 -- version check of x and the parameters
         xc, wc, aa, aw, ac, bm, sg, cbuf = ctx.bufs
         dev = xc.device
         g = grad_output.detach().to(torch.float32).contiguous()

@@ -1,5 +1,7 @@
-"""World-size-2 data-parallel exchange on gloo (CPU): the flat gradient bucket that bench.py
-all-reduces over RCCL on MI355X (cim_quantization_amd/dist.py)."""
+"""World-size-2 data parallelism on gloo (CPU): the flat gradient bucket that bench.py
+all-reduces over RCCL on MI355X, the rank-0 broadcasts that stand in for DDP's
+(examples/__init__.py:693-731), and the reference's local-batch gradient semantics,
+checked with the CPU module oracle (cim_quantization_amd/dist.py)."""
 import os
 import socket
 
@@ -17,43 +19,158 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out):
+def _run(worker, world=2):
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(worker, args=(world, port, out), nprocs=world, join=True)
+    return dict(out)
+
+
+def _init(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _gather_max_diff(t, world):
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t.contiguous())
+    return max(float((allt[0] - a).abs().max()) for a in allt[1:])
+
+
+def _exchange_worker(rank, world, port, out):
+    _init(rank, world, port)
     try:
         from cim_quantization_amd.dist import GradBucket
         torch.manual_seed(0)  # same initial parameters on every rank
         w = torch.nn.Parameter(torch.randn(16, 3, 3, 3))
         a = torch.nn.Parameter(torch.tensor([0.5]))
         bucket = GradBucket([w, a])
-        opt = torch.optim.SGD([w, a], lr=0.1, momentum=0.9)
+        opt = torch.optim.SGD([w, a], lr=0.01, momentum=0.9)
         for step in range(3):
             g = torch.Generator().manual_seed(100 * step + rank)  # different data per rank
             x = torch.randn(8, 3, 3, 3, generator=g)
+            if step == 1:
+                opt.zero_grad()  # set_to_none: autograd then writes fresh tensors, not bucket views
             loss = ((x * w.sum(0, keepdim=True)).sum() * a).square()
             loss.backward()
-            local = bucket.flat.clone()
+            local = torch.cat([w.grad.reshape(-1), a.grad.reshape(-1)]).clone()
             bucket.exchange()
+            assert w.grad.data_ptr() == bucket.views[0].data_ptr()  # re-attached
             gathered = [torch.zeros_like(local) for _ in range(world)]
             dist.all_gather(gathered, local)
             assert torch.allclose(bucket.flat, torch.stack(gathered).mean(0), rtol=1e-6, atol=1e-7)
             opt.step()
             bucket.zero()
         params = torch.cat([w.detach().reshape(-1), a.detach().reshape(-1)])
-        allp = [torch.zeros_like(params) for _ in range(world)]
-        dist.all_gather(allp, params)
-        out[rank] = float((allp[0] - allp[1]).abs().max())
+        out[rank] = (_gather_max_diff(params, world), bucket.reattached)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
 def test_bucket_exchange_world2_gloo():
-    world = 2
-    port = _free_port()
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    # every rank applied the same averaged gradients: parameters stay identical
-    assert out[0] == 0.0 and out[1] == 0.0
+    out = _run(_exchange_worker)
+    # every rank applied the same averaged gradients: parameters stay identical, and the
+    # zero_grad(set_to_none) step was caught and re-attached (2 parameters, once)
+    assert out[0] == (0.0, 2) and out[1] == (0.0, 2)
+
+
+def _broadcast_worker(rank, world, port, out):
+    _init(rank, world, port)
+    try:
+        from cim_quantization_amd import _modules as my_nn
+        from cim_quantization_amd.dist import GradBucket
+        torch.manual_seed(1234 + rank)  # deliberately different initial weights per rank
+        layers = [my_nn.Conv2dLSQCiM(16, 32, 3, 2, 1, bias=False, nbits_w=3, nbits_a=3, xbar=64, adcbits=1.5),
+                  my_nn.Conv2dLSQCiM(32, 32, 3, 1, 1, bias=False, nbits_w=3, nbits_a=3, xbar=64, adcbits=1.5)]
+        params = [p for m in layers for p in m.parameters()]
+        bucket = GradBucket(params)
+        before = _gather_max_diff(torch.cat([p.detach().reshape(-1) for p in params]), world)
+        bucket.broadcast_from(0, layers)  # construction-time sync (DDP)
+        after_setup = _gather_max_diff(torch.cat([p.detach().reshape(-1) for p in params]), world)
+        # a first training step initialises the step sizes and signed_act from the local batch
+        # (lsq.py:532-563): different on every rank ...
+        for m in layers:
+            with torch.no_grad():
+                m.alpha_act.fill_(0.1 + rank)
+                m.alpha_weight.fill_(0.2 + rank)
+                m.alpha_cim.uniform_(0.5, 1.5)
+                m.signed_act.fill_(rank)
+                m.init_state.fill_(1)
+                m.init_state_cim.fill_(1)
+        diverged = _gather_max_diff(torch.cat([p.detach().reshape(-1) for p in params]), world)
+        bucket.broadcast_from(0, layers)  # ... then re-synced from rank 0
+        synced = _gather_max_diff(torch.cat([p.detach().reshape(-1) for p in params]), world)
+        bufs = torch.cat([b.reshape(-1) for m in layers for b in m.buffers()])
+        out[rank] = (before, after_setup, diverged, synced, _gather_max_diff(bufs, world),
+                     float(layers[0].signed_act))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_broadcast_params_and_initialised_alphas_world2_gloo():
+    out = _run(_broadcast_worker)
+    for r in (0, 1):
+        before, after_setup, diverged, synced, bufs, sgn = out[r]
+        assert before > 0 and after_setup == 0.0
+        assert diverged > 0 and synced == 0.0 and bufs == 0.0
+        assert sgn == 0.0  # rank 0's signed_act everywhere
+
+
+def _local_batch_worker(rank, world, port, out):
+    _init(rank, world, port)
+    try:
+        from cim_quantization_amd.dist import GradBucket
+        from oracle.cim_module_oracle import OracleConv2dLSQCiM
+        B, C, O, H = 4, 8, 16, 8  # global batch 4 = 2 ranks x 2
+
+        def make():
+            torch.manual_seed(7)
+            m = OracleConv2dLSQCiM(C, O, 3, 1, 1, bias=False, nbits_w=3, nbits_a=3, xbar=64, adcbits=1.5)
+            with torch.no_grad():  # initialised state (one init step has happened)
+                m.alpha_act.fill_(0.13)
+                m.alpha_weight.fill_(0.21 * float(m.weight.abs().mean()))
+                m.alpha_cim.copy_(torch.rand(m.alpha_cim.shape, generator=torch.Generator().manual_seed(3)) + 0.5)
+                m.alpha_cim.mul_(0.13 * float(m.alpha_weight))
+                m.init_state.fill_(1)
+                m.init_state_cim.fill_(1)
+            return m
+
+        gen = torch.Generator().manual_seed(11)
+        x = torch.randn(B, C, H, H, generator=gen).relu()
+        gy = torch.randn(B, O, H, H, generator=gen)
+        half = B // world
+
+        def local_grads(r):
+            m = make()
+            y = m(x[r * half:(r + 1) * half])
+            y.backward(gy[r * half:(r + 1) * half])
+            return torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+
+        m = make()
+        bucket = GradBucket(list(m.parameters()))
+        m(x[rank * half:(rank + 1) * half]).backward(gy[rank * half:(rank + 1) * half])
+        bucket.exchange()
+        expect = (local_grads(0) + local_grads(1)) / 2  # DDP: mean of the per-rank local gradients
+        mf = make()
+        mf(x).backward(gy)  # single process on the global batch: ga, ps.numel() see B = 4
+        full = torch.cat([p.grad.reshape(-1) for p in mf.parameters()])
+        n_w = m.weight.numel()
+        out[rank] = (float((bucket.flat - expect).abs().max() / expect.abs().max()),
+                     float((bucket.flat[n_w:] - full[n_w:]).abs().max() / full[n_w:].abs().max()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_local_batch_semantics_world2_gloo():
+    out = _run(_local_batch_worker)
+    for r in (0, 1):
+        err_local, diff_full = out[r]
+        assert err_local < 1e-6
+        # the step-size gradients depend on the batch through ga and ps.numel() (lsq.py:323,547):
+        # averaging local gradients is NOT the global-batch gradient, as in the reference's DDP run
+        assert diff_full > 1e-3

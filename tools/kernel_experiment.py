@@ -50,7 +50,8 @@ def do_build():
     from cim_quantization_amd import build as B
     os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
     with cf.ThreadPoolExecutor(len(VARIANTS)) as ex:
-        futs = {ex.submit(B.build, True, False, lib_path(n), d): n for n, d in VARIANTS.items()}
+        futs = {ex.submit(B.build, True, False, lib_path(n), list(d) + ["CIMQ_TUNING"]): n
+                for n, d in VARIANTS.items()}
         for f in cf.as_completed(futs):
             f.result()
             print("built", futs[f], flush=True)

@@ -7,12 +7,17 @@
 
 Per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B / lane) streaming read, so
-traffic = 2 * FETCH_SIZE + WRITE_SIZE.  Output: {kernel symbol: mean bytes per dispatch}.
+traffic = 2 * FETCH_SIZE + WRITE_SIZE.  Output: {kernel symbol: mean bytes per dispatch and the
+dispatch count}, plus "_meta": the sha of the kernel sources measured (bench.py reports the
+traffic only while the sources still match).
 """
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def per_kernel(path, counter):
@@ -24,13 +29,15 @@ def per_kernel(path, counter):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         acc[k] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
-    return {k: acc[k] / len(disp[k]) for k in acc}
+    return {k: acc[k] / len(disp[k]) for k in acc}, {k: len(disp[k]) for k in acc}
 
 
-fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-write = per_kernel(sys.argv[2], "WRITE_SIZE")
-out = {}
+fetch, nf = per_kernel(sys.argv[1], "FETCH_SIZE")
+write, _ = per_kernel(sys.argv[2], "WRITE_SIZE")
+from bench import source_sha  # noqa: E402
+
+out = {"_meta": {"source_sha": source_sha()}}
 for k in sorted(set(fetch) | set(write)):
-    out[k] = {"fetch_kib": fetch.get(k), "write_kib": write.get(k),
+    out[k] = {"fetch_kib": fetch.get(k), "write_kib": write.get(k), "dispatches": nf.get(k, 0),
               "traffic_bytes": (2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024.0}
 json.dump(out, sys.stdout, indent=1)

@@ -1,5 +1,8 @@
 #!/bin/bash
-# usage: tools/sweep.sh <layer> "<ENV=.. ENV=..>" ...   -- kernel-trace one layer per env setting
+# usage: tools/sweep.sh <layer> "<CIMQ_TUNE_x=.. ...>" ...   -- kernel-trace one layer per env setting
+# (launch-shape knobs exist only in a -DCIMQ_TUNING build: tools/kernel_experiment.py --build
+#  makes exp/libcimq_base.so, which this script loads)
+export CIMQ_LIB_PATH=${CIMQ_LIB_PATH:-exp/libcimq_base.so}
 L=$1; shift
 mkdir -p gpurun_out/sweep
 n=0
