@@ -8,6 +8,7 @@ on it); fp32 division stays correctly rounded (hipcc's default).
 """
 from __future__ import annotations
 
+import concurrent.futures
 import glob
 import os
 import subprocess
@@ -29,6 +30,12 @@ def sources():
                   [os.path.join(REPO, "include", "cimq.h")])
 
 
+def units():
+    """Translation units of libcimq.so: the C-ABI entry points and the kernel-family launchers
+    (cimq_part_*.hip), compiled in parallel and linked into one shared library."""
+    return [os.path.join(CSRC, "cimq_api.hip")] + sorted(glob.glob(os.path.join(CSRC, "cimq_part_*.hip")))
+
+
 def up_to_date() -> bool:
     if not os.path.exists(OUT):
         return False
@@ -41,13 +48,29 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, defines=())
     if not force and out == OUT and up_to_date():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-munsafe-fp-atomics", "-Wno-pass-failed"]
-    cmd += [f"-D{d}" for d in defines]
-    cmd += ["-o", out + ".tmp", os.path.join(CSRC, "cimq_api.hip")]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-pass-failed"]
+    flags += [f"-D{d}" for d in defines]
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    jobs = []
+    for u in units():
+        obj = os.path.join(objdir, os.path.basename(u) + ".o")
+        jobs.append((obj, [hipcc] + flags + ["-c", "-o", obj, u]))
+
+    def run(job):
+        obj, cmd = job
+        if verbose:
+            print("[cimq] " + " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with concurrent.futures.ThreadPoolExecutor(workers) as ex:
+        objs = list(ex.map(run, jobs))
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", out + ".tmp"] + objs
     if verbose:
-        print("[cimq] " + " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        print("[cimq] " + " ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
     return out
 

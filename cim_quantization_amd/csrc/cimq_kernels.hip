@@ -164,6 +164,7 @@ __device__ inline void act_range(const Geo& g, const float* __restrict__ x, floa
   }
 }
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float* __restrict__ sa_p,
                                 const float* __restrict__ signed_p, uint8_t* __restrict__ xcf,
                                 uint8_t* __restrict__ xcb) {
@@ -172,6 +173,7 @@ __global__ void prep_act_kernel(Geo g, const float* __restrict__ x, const float*
   act_range(g, x, sa, sgn, xcf, xcb, (long long)blockIdx.x * blockDim.x + threadIdx.x,
             (long long)gridDim.x * blockDim.x);
 }
+#endif
 
 // =========================================================================================
 // prep_weight: MFMA fragments of the weight bit slices
@@ -305,6 +307,7 @@ __device__ inline void wtc_item(const Geo& g, const WSrc& ws, int Cp, uint4* __r
   wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
 }
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
                                   v4i* __restrict__ wfrag) {
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
@@ -312,7 +315,9 @@ __global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const fl
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wfrag_item(g, ws, wfrag, t);
 }
+#endif
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
                                 v4i* __restrict__ wgx) {
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
@@ -320,7 +325,9 @@ __global__ void prep_wgx_kernel(Geo g, const float* __restrict__ w_q, const floa
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wgx_item(g, ws, wgx, t);
 }
+#endif
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_wcy_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int ncpbt,
                                 v4i* __restrict__ wcy) {
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
@@ -328,7 +335,9 @@ __global__ void prep_wcy_kernel(Geo g, const float* __restrict__ w_q, const floa
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wcy_item(g, ws, ncpbt, wcy, t);
 }
+#endif
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,
                                 uint4* __restrict__ wtc) {
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
@@ -336,6 +345,7 @@ __global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const floa
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wtc_item(g, ws, Cp, wtc, t);
 }
+#endif
 
 // =========================================================================================
 // prep_params: ADC thresholds and STE intervals by exact binary search over integer ps
@@ -446,6 +456,7 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
   return literal;
 }
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, const float* __restrict__ sw_p,
                                    const float* __restrict__ sa_p, const int8_t* __restrict__ bmask,
                                    Params pp) {
@@ -455,6 +466,7 @@ __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, con
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     if (params_item(g, as, sw, sa, bmask, pp, t)) atomicOr(&pp.flags[0], 1);
 }
+#endif
 
 // =========================================================================================
 // shared tile machinery: implicit im2col of the packed act codes into LDS
@@ -848,12 +860,14 @@ __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __
   }
 }
 
+#ifdef CIMQ_TU_BWD  // non-template kernel: defined in one translation unit only
 __global__ void scale_kernel(float* __restrict__ v, long long n, const float* __restrict__ sw_p, int nba) {
   const float scale = (*sw_p) / (float)nba;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
     v[i] *= scale;
 }
+#endif
 
 // =========================================================================================
 // cim_bwd_gw: grad wrt the weights and alpha_cim; alpha_cim init   (lsq.py:321-369, 35-87)
@@ -1109,6 +1123,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
 //   y1 = x/sa ; c = clamp(y1,0,Qp) ; x_q = round_pass(c)*sa
 //   g_y1 = (0<=y1<=Qp) ? g*sa : 0 ;  g_x = g_y1/sa
 //   g_sa = sum(g*round(c)) + sum(-g_y1*((x/sa)/sa))
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void lsq_act_bwd_kernel(long long n, const float* __restrict__ x, const float* __restrict__ sa_p,
                                    float qp, float* __restrict__ gx_inout, float* __restrict__ partial) {
   __shared__ float sred[256];
@@ -1136,7 +1151,9 @@ __global__ void lsq_act_bwd_kernel(long long n, const float* __restrict__ x, con
   }
   if (threadIdx.x == 0) partial[blockIdx.x] = sred[0];
 }
+#endif
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void sum_partials_kernel(int n, const float* __restrict__ partial, float* __restrict__ out) {
   __shared__ float sred[256];
   float acc = 0.f;
@@ -1149,5 +1166,6 @@ __global__ void sum_partials_kernel(int n, const float* __restrict__ partial, fl
   }
   if (threadIdx.x == 0) out[0] = sred[0];
 }
+#endif
 
 }  // namespace cimq

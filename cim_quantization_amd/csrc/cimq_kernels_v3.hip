@@ -1486,6 +1486,7 @@ __device__ inline float reduce_chunks(const float* __restrict__ slab, size_t chu
   return v;
 }
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ __launch_bounds__(1024) void reduce_gw_v3_kernel(Geo g, int nchunks, const float* __restrict__ gw_slab,
                                                             const float* __restrict__ sa_p,
                                                             float* __restrict__ grad_w) {
@@ -1502,7 +1503,9 @@ __global__ __launch_bounds__(1024) void reduce_gw_v3_kernel(Geo g, int nchunks, 
     if (o < g.O && fl < g.xbar && f < g.K) grad_w[(size_t)o * g.K + f] = v * ((*sa_p) / (float)g.nbw);
   }
 }
+#endif
 
+#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ __launch_bounds__(1024) void reduce_galpha_v3_kernel(Geo g, int nchunks, const float* __restrict__ ga_slab,
                                                                 Params pp, float cgrad, int init,
                                                                 const float* __restrict__ sw_p,
@@ -1531,5 +1534,6 @@ __global__ __launch_bounds__(1024) void reduce_galpha_v3_kernel(Geo g, int nchun
     }
   }
 }
+#endif
 
 }  // namespace cimq
