@@ -13,11 +13,18 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
 CIMQ_LSQ_ACCUMULATE_GRADS = 1
+# cimq_conv_desc.adc_variant (include/cimq.h)
+CIMQ_ADC_LIBRARY = 0
+CIMQ_ADC_STOCHASTIC = 1
+CIMQ_ADC_SHIFT_ROUND = 2
+CIMQ_ADC_SHIFT_SIGN = 3
+CIMQ_ADC_F_PS_INT8 = 0x100
+CIMQ_ADC_F_SHIFT_RANGE = 0x200
 
 # every symbol include/cimq.h declares
 EXPORTED_SYMBOLS = (
@@ -29,6 +36,8 @@ EXPORTED_SYMBOLS = (
     "cimq_module_forward",
     "cimq_module_backward",
     "cimq_alpha_init",
+    "cimq_shift_forward",
+    "cimq_shift_backward",
     "cimq_debug_partial_sums",
     "cimq_profile_start",
     "cimq_profile_stop",
@@ -57,7 +66,9 @@ class ConvDesc(ctypes.Structure):
         ("adc_bits", ctypes.c_float),
         ("input_kind", ctypes.c_int32),
         ("lsq_qp", ctypes.c_float),
-        ("reserved", ctypes.c_int32 * 4),
+        ("adc_variant", ctypes.c_int32),
+        ("seed_lo", ctypes.c_uint32), ("seed_hi", ctypes.c_uint32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -102,6 +113,10 @@ def _bind(lib):
     lib.cimq_module_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 16
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
+    lib.cimq_shift_forward.restype = ctypes.c_int
+    lib.cimq_shift_forward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
+    lib.cimq_shift_backward.restype = ctypes.c_int
+    lib.cimq_shift_backward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 16
     lib.cimq_debug_partial_sums.restype = ctypes.c_int
     lib.cimq_debug_partial_sums.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
     lib.cimq_profile_start.restype = ctypes.c_int
@@ -140,7 +155,7 @@ def check(rc: int, what: str):
 
 
 def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w, bs_a, adc_bits,
-              input_kind=CIMQ_INPUT_XQ, lsq_qp=0.0) -> ConvDesc:
+              input_kind=CIMQ_INPUT_XQ, lsq_qp=0.0, adc_variant=CIMQ_ADC_LIBRARY, seed=0) -> ConvDesc:
     d = ConvDesc()
     d.batch, d.in_channels, d.in_h, d.in_w = int(B), int(C), int(H), int(W)
     d.out_channels, d.kernel_h, d.kernel_w = int(O), int(KH), int(KW)
@@ -151,6 +166,8 @@ def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w
     d.adc_bits = float(adc_bits)
     d.input_kind = int(input_kind)
     d.lsq_qp = float(lsq_qp)
+    d.adc_variant = int(adc_variant)
+    d.seed_lo, d.seed_hi = int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF
     return d
 
 

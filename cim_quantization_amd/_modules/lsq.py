@@ -17,7 +17,8 @@ import math
 import torch
 import torch.nn.functional as F
 
-from ..functional import alpha_cim_init, cim_conv2d_lsq, cim_module_conv, get_cim_output_signed  # noqa: F401
+from ..functional import (alpha_cim_init, cim_conv2d_lsq, cim_conv2d_lsq_shift, cim_module_conv,  # noqa: F401
+                          get_adcless_cim_output, get_analog_partial_sums_autograd_ver2, get_cim_output_signed)
 from ._quan_base import (_ActQ, _Conv2dQ, _Conv2dQCiM, _LinearQ, Qmodes, grad_scale,  # noqa: F401
                          round_pass)
 
@@ -39,15 +40,28 @@ def _adc_qp(adcbits):
 
 
 class Conv2dLSQCiM(_Conv2dQCiM):
-    """CiM-aware LSQ conv (lsq.py:511-588) on MI355X."""
+    """CiM-aware LSQ conv (lsq.py:511-588) on MI355X.
+
+    ``adc_shift=True`` (this build's option, off by default so the state_dict matches the
+    reference): a learnable per-(tile, w-slice, a-slice, channel) shift ``beta_cim`` next to
+    ``alpha_cim``, and the ADC of test/test_backward_cimlayer_scale_shift.py on the rescaled
+    partial sum u -- adcbits 1.5: clamp(round((u-beta)/alpha_q), -1, 1)*alpha_q + beta (ver2);
+    adcbits 1: sign((u-beta)/alpha_q)*alpha_q + beta (adcless).  beta starts at 0."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
                  groups=1, bias=True, nbits_w=8, nbits_a=8, nbits_alpha=8, wbitslice=1, abitslice=1,
-                 xbar=64, adcbits=6, stochastic_quant=False, **kwargs):
+                 xbar=64, adcbits=6, stochastic_quant=False, adc_shift=False, **kwargs):
         super().__init__(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
                          stride=stride, padding=padding, dilation=dilation, groups=groups, bias=bias,
                          nbits_w=nbits_w, nbits_a=nbits_a, nbits_alpha=nbits_alpha, wbitslice=wbitslice,
                          abitslice=abitslice, xbar=xbar, adcbits=adcbits, stochastic_quant=stochastic_quant)
+        self.adc_shift = bool(adc_shift)
+        if self.adc_shift:
+            if adcbits not in (1, 1.5) or stochastic_quant:
+                raise ValueError("adc_shift needs a deterministic 1- or 1.5-bit ADC (adcbits 1 / 1.5)")
+            self.beta_cim = torch.nn.Parameter(torch.zeros_like(self.alpha_cim))
+        else:
+            self.beta_cim = None
         self._state_cache = None  # host mirror of (init_state, init_state_cim) to avoid a sync per step
         self.fused = True  # steady state through cimq_module_forward/backward (False: torch quantisers)
         # parameter grads added into the existing .grad buffers inside the library (no
@@ -79,12 +93,13 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         if self.binary_mask.device != x.device:
             self.binary_mask = self.binary_mask.to(x.device)
         if (self.fused and flags[0] and (flags[1] or self.alpha_cim is None) and self.adcbits != 0
-                and not self.stochastic_quant):
+                and not self.adc_shift):
             # steady state: the three quantisers and the CiM conv in one library call each way
             out = cim_module_conv(x, self.weight, self.alpha_act, self.alpha_weight, self.alpha_cim,
                                   self.binary_mask, self.signed_act, self.stride, self.padding, self.dilation,
                                   self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
-                                  self.xbar, self.nbits_alpha, self.accumulate_grads_in_place)
+                                  self.xbar, self.nbits_alpha, self.accumulate_grads_in_place,
+                                  bool(self.stochastic_quant))
             if self.bias is not None:
                 out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
             return out
@@ -108,11 +123,14 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         if self.adcbits == 0:                                                          # lsq.py:584-585
             x_q = round_pass((x / sa).clamp(qn_a, qp_a)) * sa
             return F.conv2d(x_q, w_q, self.bias, self.stride, self.padding, self.dilation)
-        if self.stochastic_quant:
-            raise NotImplementedError("stochastic ADC (lsq.py:205-221) is not implemented on MI355X yet")
-        out = cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, self.binary_mask, self.signed_act, self.stride,
-                             self.padding, self.dilation, self.nbits_a, self.abitslice, self.nbits_w,
-                             self.wbitslice, self.adcbits, self.xbar)
+        if self.adc_shift:
+            out = cim_conv2d_lsq_shift(x, w_q, sa, sw, alpha_q, self.beta_cim, self.binary_mask, self.signed_act,
+                                       self.stride, self.padding, self.dilation, self.nbits_a, self.abitslice,
+                                       self.nbits_w, self.wbitslice, self.adcbits, self.xbar)
+        else:
+            out = cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, self.binary_mask, self.signed_act, self.stride,
+                                 self.padding, self.dilation, self.nbits_a, self.abitslice, self.nbits_w,
+                                 self.wbitslice, self.adcbits, self.xbar, bool(self.stochastic_quant))
         fold_x = int((x.shape[-1] - self.weight.shape[-1] + 2 * self.padding[0]) / self.stride[0] + 1)
         out = out.transpose(1, 2).view(x.shape[0], self.out_channels, fold_x, fold_x)  # lsq.py:580-581
         if self.bias is not None:

@@ -11,7 +11,7 @@ namespace {
 
 int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, const float* sw,
              const float* alpha_q, const int8_t* bmask, const float* signed_act, uint8_t* ctx,
-             hipStream_t s, bool need_params, bool need_wgx) {
+             hipStream_t s, bool need_params, bool need_wgx, const float* beta = nullptr) {
   CtxLayout L = ctx_layout(g);
   const int blk = 256;
   {
@@ -52,7 +52,7 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     if (hipMemsetAsync(pp.flags, 0, 16, s) != hipSuccess) return fail(CIMQ_EHIP, "memset flags");
     int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
     hipLaunchKernelGGL(prep_params_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, alpha_q, sw, sa,
-                       bmask, pp);
+                       bmask, pp, beta);
     CIMQ_TRY(check_hip("prep_params"));
   }
   return CIMQ_OK;
@@ -79,6 +79,17 @@ int launch_reduce_galpha(const Geo& g, const uint8_t* ctx, uint8_t* ws, float cg
                      reinterpret_cast<const float*>(ws + W.ga_slab), params_of(g, const_cast<uint8_t*>(ctx)),
                      cgrad, init, sw, sa, (float)((double)g.B * g.P), (float)sqrt((double)g.qp), out);
   return check_hip("reduce_galpha");
+}
+
+// mask * cgrad * (slab sum over the backward's pixel chunks) -> [1, T, nbw, nba, 1, O]
+int launch_reduce_slab(const Geo& g, const uint8_t* ctx, uint8_t* ws, size_t slab, float cgrad, const float* sw,
+                       const float* sa, float* out, hipStream_t s) {
+  WsLayout W = ws_layout(g);
+  const long long nout = (long long)g.T * g.nbw * g.nba * g.Opad;
+  hipLaunchKernelGGL(reduce_galpha_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks_bwd,
+                     reinterpret_cast<const float*>(ws + slab), params_of(g, const_cast<uint8_t*>(ctx)), cgrad, 0,
+                     sw, sa, 1.f, 1.f, out);
+  return check_hip("reduce_slab");
 }
 
 }  // namespace
@@ -109,11 +120,72 @@ int cimq_forward(const cimq_conv_desc* d, const float* x, const float* w_q, cons
     return fail(CIMQ_EINVAL, "null pointer argument");
   if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && !alpha_q)
     return fail(CIMQ_EINVAL, "adc_bits 1 / 1.5 need alpha_q");
+  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
+    return fail(CIMQ_EINVAL, "scale/shift ADC variants go through cimq_shift_forward");
   (void)ws;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
   CIMQ_TRY(prep_all(g, x, w_q, sa, sw, alpha_q, binary_mask, signed_act, c, s, true, true));
   return launch_fwd_any(g, c, sw, sa, out, nullptr, nullptr, s);
+}
+
+int cimq_shift_forward(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                       const float* sw, const float* alpha, const float* beta, const int8_t* binary_mask,
+                       const float* signed_act, float* out, void* ctx, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (g.variant != VAR_SHIFT_ROUND && g.variant != VAR_SHIFT_SIGN)
+    return fail(CIMQ_EINVAL, "cimq_shift_forward needs adc_variant CIMQ_ADC_SHIFT_ROUND or _SIGN");
+  if (!x || !w_q || !sa || !sw || !alpha || !beta || !binary_mask || !signed_act || !out || !ctx)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  (void)ws;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
+  CIMQ_TRY(prep_all(g, x, w_q, sa, sw, alpha, binary_mask, signed_act, c, s, true, true, beta));
+  return launch_fwd_any(g, c, sw, sa, out, nullptr, nullptr, s);
+}
+
+int cimq_shift_backward(const cimq_conv_desc* d, const float* grad_out, const float* x, const float* sa,
+                        const float* sw, const float* alpha, const float* beta, const int8_t* binary_mask,
+                        const float* signed_act, const void* ctx, float* grad_x, float* grad_w,
+                        float* grad_alpha, float* grad_beta, float* grad_sa, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  (void)alpha; (void)beta; (void)binary_mask;
+  if (g.variant != VAR_SHIFT_ROUND && g.variant != VAR_SHIFT_SIGN)
+    return fail(CIMQ_EINVAL, "cimq_shift_backward needs adc_variant CIMQ_ADC_SHIFT_ROUND or _SIGN");
+  if (!grad_out || !sa || !sw || !signed_act || !ctx || !grad_x || !grad_w || !grad_alpha || !grad_beta || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if (g.input_kind == CIMQ_INPUT_RAW_LSQ && (!x || !grad_sa))
+    return fail(CIMQ_EINVAL, "RAW_LSQ backward needs x and grad_sa");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  bool lsq_fused = false;
+  CIMQ_TRY(launch_bwd_general(g, c, sw, sa, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
+  WsLayout W = ws_layout(g);
+  {
+    const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
+    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks_bwd,
+                       reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
+    CIMQ_TRY(check_hip("reduce_gw"));
+  }
+  // grad_alpha: sign variant sum sign * G / sqrt(numel * Qp) (scale_shift.py:283); round variant
+  // without the factor (:491 commented out); grad_beta: sum over the clamped region / all of G
+  const double numel = (double)g.B * g.T * g.nbw * g.nba * g.P * g.O;
+  const float cgrad = g.variant == VAR_SHIFT_SIGN ? (float)(1.0 / sqrt(numel * (double)g.qp)) : 1.f;
+  CIMQ_TRY(launch_reduce_slab(g, c, w, W.ga_slab, cgrad, sw, sa, grad_alpha, s));
+  CIMQ_TRY(launch_reduce_slab(g, c, w, W.gb_slab, 1.f, sw, sa, grad_beta, s));
+  if (g.input_kind == CIMQ_INPUT_RAW_LSQ) {
+    float* part = reinterpret_cast<float*>(w + W.lsq_part);
+    int grid = cdiv(g.Nin, 256);
+    if (grid > kLsqParts) grid = kLsqParts;
+    hipLaunchKernelGGL(lsq_act_bwd_kernel, dim3(grid), dim3(256), 0, s, g.Nin, x, sa, g.lsq_qp, grad_x, part);
+    CIMQ_TRY(check_hip("lsq_act_bwd"));
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, grid, part, grad_sa);
+    CIMQ_TRY(check_hip("sum_partials"));
+  }
+  return CIMQ_OK;
 }
 
 int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
@@ -141,6 +213,8 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   (void)alpha_q; (void)binary_mask;
   if (!grad_out || !sa || !sw || !signed_act || !ctx || !grad_x || !grad_w || !ws)
     return fail(CIMQ_EINVAL, "null pointer argument");
+  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
+    return fail(CIMQ_EINVAL, "scale/shift ADC variants go through cimq_shift_backward");
   if (g.input_kind == CIMQ_INPUT_RAW_LSQ && (!x || !grad_sa))
     return fail(CIMQ_EINVAL, "RAW_LSQ backward needs x and grad_sa");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -202,6 +276,8 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   Geo g;
   CIMQ_TRY(make_geo(d, &g));
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
+    return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
   LsqArgs la;
   CIMQ_TRY(lsq_args(g, q, &la));
   if (!x || !weight || !alpha_act || !alpha_weight || !binary_mask || !signed_act || !out || !ctx || !ws)
@@ -268,6 +344,8 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
   Geo g;
   CIMQ_TRY(make_geo(d, &g));
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
+    return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
   LsqArgs la;
   CIMQ_TRY(lsq_args(g, q, &la));
   (void)alpha_act; (void)alpha_weight; (void)binary_mask;

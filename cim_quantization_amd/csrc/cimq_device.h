@@ -15,6 +15,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 
 enum AdcMode { ADC_FP = 0, ADC_SIGN = 1, ADC_TERNARY = 2, ADC_MULTI = 3 };
+// cimq_conv_desc.adc_variant & 0xFF (include/cimq.h CIMQ_ADC_*)
+enum AdcVariant { VAR_LIBRARY = 0, VAR_STOCHASTIC = 1, VAR_SHIFT_ROUND = 2, VAR_SHIFT_SIGN = 3 };
 
 // Problem geometry, computed once on the host (cimq_api.hip) and passed by value.
 struct Geo {
@@ -31,6 +33,9 @@ struct Geo {
   int psmax;               // bound on |partial sum| used by the threshold search
   long long Nin;           // B*C*H*W
   int onchw;               // out / grad_out layout: 0 = [B, P, O] (the Function's), 1 = NCHW (the module's)
+  int variant;             // AdcVariant; anything but VAR_LIBRARY runs the literal (general) kernels
+  int ps_int8;             // partial sums pass an int8 buffer before the ADC (scale_shift.py:401)
+  uint32_t seed_lo, seed_hi;  // VAR_STOCHASTIC: Philox key
 };
 
 // Per-(tile i, a-slice j, w-slice k, out-channel o) ADC / STE parameters, SoA.
@@ -44,6 +49,7 @@ struct Params {
   float* alpha; // alpha_q (literal paths)
   float* ckj;   // [3][nbw*nba]: mask as float, cE = 2^-(bsa*j)*mask, cD = 2^-(bsw*k)*mask
   int* flags;   // [0]: literal ADC (degenerate alpha / scales), [1..3] reserved
+  float* beta;  // shift of the scale + shift ADC variants (0 otherwise)
 };
 
 __host__ __device__ inline int pidx(const Geo& g, int i, int j, int k, int o) {
@@ -161,6 +167,112 @@ __device__ inline float alpha_code_literal(float psb, int mode, float qn, float 
   if (psb >= thr_hi) q = qp;
   if (psb <= thr_lo) q = qn;
   return q;
+}
+
+// ---------------------------------------------------------------------------------------
+// ADC variants (cimq_conv_desc.adc_variant), evaluated literally per partial sum
+// ---------------------------------------------------------------------------------------
+__device__ inline bool has_alpha(const Geo& g) {
+  return g.mode == ADC_SIGN || g.mode == ADC_TERNARY || g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN;
+}
+__device__ inline bool is_shift(const Geo& g) { return g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN; }
+
+// torch.sign: NaN propagates
+__device__ inline float sign_nan(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : ((v != v) ? v : 0.f)); }
+
+// the partial sum as the ADC input sees it, times sw * sa (lsq.py:195): the fp16 store of the
+// library (lsq.py:169) or the int8 buffer of the scale/shift ver2 Function (scale_shift.py:401)
+__device__ inline float u_var(const Geo& g, int p, float sw, float sa) {
+  float ps = ps_half(p);
+  if (g.ps_int8) ps = (float)(int8_t)(((int)ps) & 0xFF);
+  const float t = ps * sw;
+  return t * sa;
+}
+
+// Philox4x32-10 (Salmon et al., SC'11): counter-based, so a draw depends only on (key, counter)
+__device__ inline void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// number of draws U ~ [0,1) (24-bit) with ceil(s - U) == 1, i.e. U < s, out of 50 (lsq.py:214-217);
+// draws d = 0..49 of stream `which` of element `eid`
+__device__ inline float bernoulli50(float s, uint64_t eid, uint32_t which, uint32_t k0, uint32_t k1) {
+  if (s <= 0.f) return 0.f;   // ceil(0 - U) = 0 for every U in [0, 1)
+  if (s >= 1.f) return 50.f;  // ceil(1 - U) = 1
+  float n = 0.f;
+  for (uint32_t blk = 0; blk < 13; ++blk) {
+    uint32_t c[4] = {(uint32_t)eid, (uint32_t)(eid >> 32), which, blk};
+    philox4x32(c, k0, k1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (blk * 4 + e < 50) {
+        const float u = (float)(c[e] >> 8) * 5.9604644775390625e-8f;  // 2^-24
+        n += (s - u > 0.f) ? 1.f : 0.f;                                // ceil(s - u) with s - u in (-1, 1)
+      }
+    }
+  }
+  return n;
+}
+
+// stochastic 1.5-bit ADC of lsq.py:205-221 for one partial sum (u = ps*sw*sa)
+__device__ inline float adc_stochastic(const Geo& g, float u, float alpha, uint64_t eid) {
+  const float h = 0.5f * alpha;
+  const float z1 = (u - h) / 0.01f, z2 = (u + h) / 0.01f;
+  const float s1 = 1.f / (1.f + expf(-z1)), s2 = 1.f / (1.f + expf(-z2));  // torch.sigmoid
+  const float n1 = bernoulli50(s1, eid, 0u, g.seed_lo, g.seed_hi);
+  const float n2 = bernoulli50(s2, eid, 1u, g.seed_lo, g.seed_hi);
+  const float a = n1 / 50.f, b = n2 / 50.f;
+  const float v = (a + b) - 1.f;
+  return clamp_nan(rintf(v), g.qn, g.qp) * alpha;
+}
+
+// ADC output (before the shift-and-add mask) of one partial sum, every variant
+__device__ inline float adc_value(const Geo& g, int p, float sw, float sa, float alpha, float beta, uint64_t eid) {
+  if (g.variant == VAR_SHIFT_ROUND) {
+    const float v = (u_var(g, p, sw, sa) - beta) / alpha;  // scale_shift.py:421
+    const float t = clamp_nan(rintf(v), g.qn, g.qp) * alpha;  // :424-425
+    return t + beta;
+  }
+  if (g.variant == VAR_SHIFT_SIGN) {
+    const float v = (u_var(g, p, sw, sa) - beta) / alpha;  // scale_shift.py:202
+    const float t = sign_nan(v) * alpha;                    // :209-211
+    return t + beta;
+  }
+  if (g.variant == VAR_STOCHASTIC) return adc_stochastic(g, u_of(p, sw, sa), alpha, eid);
+  return adc_literal(p, g.mode, sw, sa, alpha, g.qn, g.qp);
+}
+
+// the backward's rescaled partial sum (lsq.py:257-267; scale_shift.py:469 / :202)
+__device__ inline float psb_value(const Geo& g, int p, float sw, float sa, float alpha, float beta) {
+  if (is_shift(g)) return (u_var(g, p, sw, sa) - beta) / alpha;
+  return psb_literal(p, g.mode, sw, sa, alpha);
+}
+
+// per-partial-sum factor of grad_alpha (times g, summed over the batch and pixels)
+__device__ inline float alpha_term(const Geo& g, float b) {
+  if (g.variant == VAR_SHIFT_ROUND) {  // scale_shift.py:488-495: round(ps) - ps, Qp / Qn where clamped
+    if (b >= g.thr_hi) return g.qp;
+    if (b <= g.thr_lo) return g.qn;
+    return rintf(b) - b;
+  }
+  if (g.variant == VAR_SHIFT_SIGN) return sign_nan(b);  // scale_shift.py:281
+  return alpha_code_literal(b, g.mode, g.qn, g.qp, g.thr_hi, g.thr_lo);
+}
+
+// per-partial-sum factor of grad_beta: the clamped region (ver2, :496-501) or 1 (adcless, :287)
+__device__ inline float beta_term(const Geo& g, float b) {
+  if (g.variant == VAR_SHIFT_SIGN) return 1.f;
+  return (b >= g.thr_hi || b <= g.thr_lo) ? 1.f : 0.f;
 }
 
 // fp32 -> bf16 round-to-nearest-even (finite inputs) and back

@@ -112,6 +112,33 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
   if (g.input_kind != CIMQ_INPUT_XQ && g.input_kind != CIMQ_INPUT_RAW_LSQ)
     return fail(CIMQ_EINVAL, "bad input_kind");
   g.lsq_qp = d->lsq_qp;
+  g.variant = d->adc_variant & 0xFF;
+  if (d->adc_variant & ~(0xFF | CIMQ_ADC_F_PS_INT8 | CIMQ_ADC_F_SHIFT_RANGE))
+    return fail(CIMQ_EINVAL, "unknown adc_variant flags 0x%x", d->adc_variant);
+  g.ps_int8 = (d->adc_variant & CIMQ_ADC_F_PS_INT8) ? 1 : 0;
+  g.seed_lo = d->seed_lo;
+  g.seed_hi = d->seed_hi;
+  switch (g.variant) {
+    case VAR_LIBRARY: break;
+    case VAR_STOCHASTIC:  // lsq.py:136-137: the stochastic ADC is the 1.5-bit one
+      if (g.mode != ADC_TERNARY) return fail(CIMQ_EINVAL, "the stochastic ADC needs adc_bits 1.5");
+      break;
+    case VAR_SHIFT_SIGN:
+      if (ab != 1.f) return fail(CIMQ_EINVAL, "the scale/shift sign ADC needs adc_bits 1");
+      break;
+    case VAR_SHIFT_ROUND:
+      if (g.mode == ADC_FP) return fail(CIMQ_EINVAL, "the scale/shift ADC needs adc_bits >= 1");
+      break;
+    default: return fail(CIMQ_EINVAL, "unknown adc_variant %d", g.variant);
+  }
+  if ((d->adc_variant & CIMQ_ADC_F_SHIFT_RANGE) && ab != 1.f) {
+    // scale_shift.py:369-375: Qp = 2^(b-1) - 1, Qn = -2^(b-1) (also for 1.5 bits)
+    qp = pow(2.0, (double)ab - 1.0) - 1.0;
+    qn = -pow(2.0, (double)ab - 1.0);
+    g.qp = (float)qp; g.qn = (float)qn;
+    g.thr_hi = (float)(qp + 1e-5);
+    g.thr_lo = (float)(qn - 1e-5);
+  }
   long long psmax = (long long)tmax * (1LL << g.bsa) * (1LL << g.bsw);
   g.psmax = (int)(psmax > (1 << 24) ? (1 << 24) : psmax);
   *out = g;
@@ -119,7 +146,7 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 }
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t total;
 };
@@ -140,6 +167,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.mhi = o; o = align256(o + npar * 4);
   L.coef = o; o = align256(o + npar * 4);
   L.alpha = o; o = align256(o + npar * 4);
+  L.beta = o; o = align256(o + npar * 4);
   L.ckj = o; o = align256(o + 3 * 64 * 4);
   L.flags = o; o = align256(o + 16);
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
@@ -161,6 +189,7 @@ inline Params params_of(const Geo& g, uint8_t* base) {
   p.mhi = reinterpret_cast<int*>(base + L.mhi);
   p.coef = reinterpret_cast<float*>(base + L.coef);
   p.alpha = reinterpret_cast<float*>(base + L.alpha);
+  p.beta = reinterpret_cast<float*>(base + L.beta);
   p.ckj = reinterpret_cast<float*>(base + L.ckj);
   p.flags = reinterpret_cast<int*>(base + L.flags);
   return p;
@@ -183,7 +212,7 @@ inline size_t lds_tile(const Geo& g) {
   return align256((size_t)g.nba * 64 * g.KTP + 2 * sizeof(int) * g.KS * 64 + sizeof(int4) * 64);
 }
 inline size_t lds_gw(const Geo& g) {
-  return lds_tile(g) + sizeof(float) * g.nbw * g.nba * 32 + sizeof(float) * g.FBT * 16 * 32 +
+  return lds_tile(g) + 2 * sizeof(float) * g.nbw * g.nba * 32 + sizeof(float) * g.FBT * 16 * 32 +
          (size_t)g.nba * g.KS * 64 * 64;
 }
 const size_t kLdsMax = 160 * 1024;
@@ -207,6 +236,7 @@ inline Plan3 v3_plan(const Geo& g) {
   Plan3 p;
   memset(&p, 0, sizeof(p));
   if (tune("V3", 1) == 0) return p;  // experiments: force the general kernels
+  if (g.variant != VAR_LIBRARY) return p;  // ADC variants: literal per-partial-sum evaluation
   if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0 || g.Wo < 4) return p;
   if (g.O > 256 || 256 % g.O != 0) return p;  // grad_alpha reducer: one thread per channel
   if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
@@ -359,7 +389,7 @@ inline Plan7 v7_plan(const Geo& g) {
 }
 
 struct WsLayout {
-  size_t gw_slab, ga_slab, lsq_part, gaq, wpart, bpo, total;
+  size_t gw_slab, ga_slab, gb_slab, lsq_part, gaq, wpart, bpo, total;
   int rows, nchunks, nchunks_bwd;
 };
 
@@ -374,6 +404,8 @@ inline WsLayout ws_layout(const Geo& g) {
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
   W.ga_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad);
+  W.gb_slab = o; o = align256(o + (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN
+                                       ? sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad : 0));
   W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * g.H));  // >= B * bands
   // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
   // a [B, P, O] staging copy of out / grad_out for the general kernels

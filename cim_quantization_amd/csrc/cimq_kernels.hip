@@ -397,7 +397,8 @@ __device__ inline bool scales_ok(float sw, float sa) {
 // one (i, j, k, o) entry (t < npar) or one (k, j) coefficient triple (t >= npar); returns
 // whether the entry needs the literal ADC
 __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float sa,
-                                   const int8_t* __restrict__ bmask, const Params& pp, int t) {
+                                   const int8_t* __restrict__ bmask, const Params& pp, int t,
+                                   const float* __restrict__ beta = nullptr) {
   const int npar = g.T * g.nba * g.nbw * g.Opad;
   const int nkj = g.nbw * g.nba;
   if (t >= npar) {  // per-(k,j) float coefficients
@@ -415,9 +416,10 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
   const int i = r / g.nba;
   const float mk = (float)bmask[k * g.nba + j];
   float a = 1.f;
-  if ((g.mode == ADC_SIGN || g.mode == ADC_TERNARY) && as.a != nullptr && o < g.O)
+  if (has_alpha(g) && as.a != nullptr && o < g.O)
     a = as.get(((i * g.nbw + k) * g.nba + j) * g.O + o);  // alpha[0,i,k,j,0,o]
   pp.alpha[t] = a;
+  pp.beta[t] = (beta != nullptr && o < g.O) ? beta[((i * g.nbw + k) * g.nba + j) * g.O + o] : 0.f;
   pp.coef[t] = a * mk;
   const int lo = -g.psmax - 1, hi = g.psmax + 1;
   bool literal = false;
@@ -425,6 +427,7 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
   if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
     if (!(scales_ok(sw, sa) && a > 0.f && isfinite(a))) literal = true;
   }
+  if (g.variant != VAR_LIBRARY) literal = true;  // the variants are evaluated per partial sum
   if (!literal) {
     if (g.mode == ADC_TERNARY) {
       thi = first_true_ternary_hi(lo, hi, sw, sa, a);
@@ -459,12 +462,12 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
 #ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, const float* __restrict__ sw_p,
                                    const float* __restrict__ sa_p, const int8_t* __restrict__ bmask,
-                                   Params pp) {
+                                   Params pp, const float* __restrict__ beta) {
   const float sw = *sw_p, sa = *sa_p;
   const ASrc as{alpha_q, 0, 0.f, 0.f};
   const int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
-    if (params_item(g, as, sw, sa, bmask, pp, t)) atomicOr(&pp.flags[0], 1);
+    if (params_item(g, as, sw, sa, bmask, pp, t, beta)) atomicOr(&pp.flags[0], 1);
 }
 #endif
 
@@ -594,7 +597,7 @@ __global__ __launch_bounds__(256) void cim_fwd_kernel(Geo g, const int8_t* __res
   const int og = blockIdx.y;
   const int nob = min(4, g.OB16 - og * 4);
   const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0) || g.mode != ADC_TERNARY;
+  const bool literal = (pp.flags[0] != 0) || g.mode != ADC_TERNARY || g.variant != VAR_LIBRARY;
   const int nkj = g.nbw * g.nba;
 
   build_rowinfo(g, m0, sm.rowinfo);
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(256) void cim_fwd_kernel(Geo g, const int8_t* __res
                     const float q = (acc[r] >= pp.thi[pi]) ? 1.f : ((acc[r] <= pp.tlo[pi]) ? -1.f : 0.f);
                     adc = q * pp.alpha[pi];
                   } else {
-                    adc = adc_literal(acc[r], g.mode, sw, sa, pp.alpha[pi], g.qn, g.qp);
+                    adc = adc_value(g, acc[r], sw, sa, pp.alpha[pi], pp.beta[pi], (uint64_t)di);
                   }
                   adc_dbg[di] = adc;
                 }
@@ -660,10 +663,16 @@ __global__ __launch_bounds__(256) void cim_fwd_kernel(Geo g, const int8_t* __res
                 acc_out[ob][r] += v;
               }
             } else {
-              const float al = pp.alpha[pi];
+              const float al = pp.alpha[pi], be = pp.beta[pi];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float adc = adc_literal(acc[r], g.mode, sw, sa, al, g.qn, g.qp);
+                uint64_t eid = 0;  // element id of the stochastic ADC's draws: [B, T, nbw, nba, P, O] order
+                if (g.variant == VAR_STOCHASTIC) {
+                  const int m = m0 + wave * 16 + 4 * g4 + r;
+                  const int b = m / g.P, p = m - b * g.P;
+                  eid = ((((uint64_t)b * g.T + i) * g.nbw + k) * g.nba + j) * (uint64_t)g.P * g.O + (uint64_t)p * g.O + o;
+                }
+                const float adc = adc_value(g, acc[r], sw, sa, al, be, eid);
                 acc_out[ob][r] += adc * mk;
               }
             }
@@ -715,7 +724,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0);
+  const bool literal = (pp.flags[0] != 0) || g.variant != VAR_LIBRARY;
   const int nkj = g.nbw * g.nba;
   const int chw = g.C * g.HW;
 
@@ -778,7 +787,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __
                 if (!literal) {
                   pass = (unsigned)(acc[r] - pp.mlo[pi + r]) <= (unsigned)pp.mhi[pi + r];
                 } else {
-                  const float b = psb_literal(acc[r], g.mode, sw, sa, pp.alpha[pi + r]);
+                  const float b = psb_value(g, acc[r], sw, sa, pp.alpha[pi + r], pp.beta[pi + r]);
                   pass = ste_pass(b, g.thr_hi, g.thr_lo);
                 }
                 E[kk][r] += pass ? ce : 0.f;
@@ -888,7 +897,8 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                                                          const float* __restrict__ signed_p,
                                                          const float* __restrict__ gout, int rows_per_chunk,
                                                          float* __restrict__ gw_slab,
-                                                         float* __restrict__ ga_slab) {
+                                                         float* __restrict__ ga_slab,
+                                                         float* __restrict__ gb_slab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   TileSmem sm;
   sm.As = reinterpret_cast<int8_t*>(smem);
@@ -906,6 +916,8 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   off += sizeof(float) * nkj * ncol;
   float* gwacc = reinterpret_cast<float*>(smem + off);  // [FBT*16][32]
   off += sizeof(float) * g.FBT * 16 * ncol;
+  float* qbacc = reinterpret_cast<float*>(smem + off);  // [nkj][32]: sum beta_term*g (shift variants)
+  off += sizeof(float) * nkj * ncol;
   int8_t* Xb = reinterpret_cast<int8_t*>(smem + off);   // [nba][tlen][64] bwd slices, f-major
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -916,11 +928,14 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const int mc = blockIdx.x;
   const int mbeg = mc * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
   const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0);
+  const bool literal = (pp.flags[0] != 0) || g.variant != VAR_LIBRARY;
   const bool ternary_fast = (!literal) && g.mode == ADC_TERNARY;
-  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
+  const bool has_code = has_alpha(g);
+  const bool shift = is_shift(g);
 
   for (int t = threadIdx.x; t < nkj * ncol * (INIT ? 4 : 1); t += blockDim.x) qacc[t] = 0.f;
+  if (!INIT)
+    for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) qbacc[t] = 0.f;
   if (!INIT)
     for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
   v4f gwa[FBMAX][2];
@@ -992,7 +1007,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                       xa[ks], wfrag[((size_t)(i * g.KS + ks) * g.NBLK + nb) * WAVE + lane], acc, 0, 0, 0);
               const int pi = pidx(g, i, j, k, o);
               const int kj = k * g.nba + j;
-              float qs = 0.f;
+              float qs = 0.f, qb = 0.f;
               if (INIT) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1011,25 +1026,31 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                     qs += q * gval[r];
                   }
                 } else {
-                  const float al = pp.alpha[pi];
+                  const float al = pp.alpha[pi], be = pp.beta[pi];
                   const int mlo = pp.mlo[pi], mhi = pp.mhi[pi];
 #pragma unroll
                   for (int r = 0; r < 4; ++r) {
                     const int p = acc[r];
-                    const float b = psb_literal(p, g.mode, sw, sa, al);
+                    const float b = psb_value(g, p, sw, sa, al, be);
                     const bool pass = literal ? ste_pass(b, g.thr_hi, g.thr_lo) : ((unsigned)(p - mlo) <= (unsigned)mhi);
                     D[j][r] += pass ? cd : 0.f;
-                    if (has_code) qs += alpha_code_literal(b, g.mode, g.qn, g.qp, g.thr_hi, g.thr_lo) * gval[r];
+                    if (has_code) qs += alpha_term(g, b) * gval[r];
+                    if (shift) qb += beta_term(g, b) * gval[r];
                   }
                 }
               }
               // lanes l, l^16, l^32, l^48 share the column: fold the 16 pixel rows, then LDS
               qs += __shfl_xor(qs, 16);
               qs += __shfl_xor(qs, 32);
+              if (shift) {
+                qb += __shfl_xor(qb, 16);
+                qb += __shfl_xor(qb, 32);
+              }
               if (INIT) {
                 if (g4 == 0) qacc[(wave * nkj + kj) * ncol + ocol] += qs;
               } else if (g4 == 0 && has_code) {
                 atomicAdd(&qacc[kj * ncol + ocol], qs);
+                if (shift) atomicAdd(&qbacc[kj * ncol + ocol], qb);
               }
             }
           }
@@ -1107,6 +1128,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
       float qv = qacc[t];
       if (INIT) qv = ((qv + qacc[nkj * ncol + t]) + qacc[2 * nkj * ncol + t]) + qacc[3 * nkj * ncol + t];
       ga_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qv;
+      if (!INIT && shift) gb_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qbacc[t];
     }
   }
   if (INIT) return;

@@ -43,7 +43,7 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
                        reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(ctx + L.wfrag),
                        pp, sw, sa, signed_act, gout, W.rows, reinterpret_cast<float*>(ws + W.gw_slab),
-                       reinterpret_cast<float*>(ws + W.ga_slab));
+                       reinterpret_cast<float*>(ws + W.ga_slab), reinterpret_cast<float*>(ws + W.gb_slab));
   }
   prof_end(slot, s);
   return check_hip("cim_bwd_gw");

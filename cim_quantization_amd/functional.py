@@ -6,6 +6,11 @@
 ``cim_conv2d_lsq``         the fused path used by ``Conv2dLSQCiM``: the activation LSQ
                            quantiser (lsq.py:547-549) runs inside the CiM kernels, so x_q
                            is never materialised; grads flow to x and to the step size sa.
+``get_analog_partial_sums_autograd_ver2`` / ``get_adcless_cim_output``
+                           drop-ins for the scale + shift ADC Functions of
+                           test/test_backward_cimlayer_scale_shift.py (:336-546 / :113-334):
+                           same 14 positional args, grads for x, w, alpha_cim, beta_cim.
+``cim_conv2d_lsq_shift``   the scale + shift ADC as a Conv2dLSQCiM option (adc_shift=True).
 
 Device-only: CPU tensors raise (there is no CPU fallback in the product path).
 """
@@ -27,6 +32,13 @@ def _require_device(*ts):
 
 def _stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+def stochastic_seed() -> int:
+    """Philox key of one stochastic-ADC call, drawn from torch's default CPU generator: the
+    draws are reproducible under ``torch.manual_seed`` (the reference draws torch.cuda
+    uniform_ noise, lsq.py:215-216) and no device synchronisation is needed."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
 
 
 def _f32(t, device):
@@ -57,12 +69,13 @@ class get_cim_output_signed(torch.autograd.Function):
                 weight_scaling_factor, act_scaling_factor, stochastic, signed_act):
         if stochastic:
             assert adc_bits == 1.5  # lsq.py:136-137
-            raise NotImplementedError("stochastic ADC (lsq.py:205-221) is not implemented on MI355X yet")
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, w, conv_stride, conv_padding, conv_dilation)
         desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, arr, weight_bits, act_bits,
-                              weight_bit_slice, act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ)
+                              weight_bit_slice, act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ,
+                              adc_variant=_lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
+                              seed=stochastic_seed() if stochastic else 0)
         sizes = _lib.query_sizes(desc)
         xq = x.detach().to(torch.float32).contiguous()
         wq = w.detach().to(torch.float32).contiguous()
@@ -110,13 +123,15 @@ class _CimConv2dLSQ(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding, dilation,
-                nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
+                nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, stochastic=False):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, w_q, stride, padding, dilation)
         qp_a = float(2 ** nbits_a - 1)
         desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
-                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a)
+                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a,
+                              _lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
+                              stochastic_seed() if stochastic else 0)
         sizes = _lib.query_sizes(desc)
         xc = x.detach().to(torch.float32).contiguous()
         wq = w_q.detach().to(torch.float32).contiguous()
@@ -157,14 +172,175 @@ class _CimConv2dLSQ(torch.autograd.Function):
                                      cbuf.data_ptr(), gx.data_ptr(), gw.data_ptr(),
                                      None if ga is None else ga.data_ptr(), gsa.data_ptr(), ws.data_ptr(),
                                      _stream()), "cimq_backward")
-        return (gx, gw, gsa, None, ga) + (None,) * 11
+        return (gx, gw, gsa, None, ga) + (None,) * 12
 
 
 def cim_conv2d_lsq(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding, dilation,
-                   nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
-    """out[B, P, O] of the fused act-LSQ + CiM conv; differentiable in x, w_q, sa, alpha_q."""
+                   nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, stochastic=False):
+    """out[B, P, O] of the fused act-LSQ + CiM conv; differentiable in x, w_q, sa, alpha_q.
+    ``stochastic``: the stochastic 1.5-bit ADC of lsq.py:205-221 in the forward."""
     return _CimConv2dLSQ.apply(x, w_q, sa, sw, alpha_q, binary_mask, signed_act, stride, padding,
-                               dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar)
+                               dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, stochastic)
+
+
+# ---------------------------------------------------------------------------------------------
+# scale + shift ADC (test/test_backward_cimlayer_scale_shift.py)
+# ---------------------------------------------------------------------------------------------
+def _mask_int8(binary_mask, dev):
+    bm = binary_mask.detach().to(device=dev)
+    b8 = bm.to(torch.int8)
+    if not torch.equal(b8.to(bm.dtype), bm):
+        raise ValueError("binary_mask values must be int8 integers (as _Conv2dQCiM builds them)")
+    return b8.contiguous()
+
+
+def _shift_forward(ctx, x, w, sa, sw, alpha, beta, binary_mask, signed_act, stride, padding, dilation,
+                   act_bits, act_bs, w_bits, w_bs, adc_bits, arr, variant, input_kind, qp_a):
+    _require_device(x)
+    dev = x.device
+    B, C, H, W, O, KH, KW, st, pd = _geometry(x, w, stride, padding, dilation)
+    desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, arr, w_bits, act_bits, w_bs, act_bs, adc_bits,
+                          input_kind, qp_a, variant)
+    sizes = _lib.query_sizes(desc)
+    xc = x.detach().to(torch.float32).contiguous()
+    wc = w.detach().to(torch.float32).contiguous()
+    sa_ = _f32(sa, dev).reshape(-1)[:1].contiguous()
+    sw_ = _f32(sw, dev).reshape(-1)[:1].contiguous()
+    al = _f32(alpha, dev)
+    be = _f32(beta, dev)
+    T = num_xbars(C, (KH, KW), arr)
+    nbw, nba = int(w_bits / w_bs), int(act_bits / act_bs)
+    if al.numel() != T * nbw * nba * O or be.numel() != T * nbw * nba * O:
+        al = al.expand(1, T, nbw, nba, 1, O).contiguous()
+        be = be.expand(1, T, nbw, nba, 1, O).contiguous()
+    bm = _mask_int8(binary_mask, dev)
+    sg = _f32(signed_act, dev).reshape(-1)[:1].contiguous()
+    Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+    Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+    out = torch.empty(B, Ho * Wo, O, device=dev, dtype=torch.float32)
+    cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+    lib = _lib.load()
+    _lib.check(lib.cimq_shift_forward(desc, xc.data_ptr(), wc.data_ptr(), sa_.data_ptr(), sw_.data_ptr(),
+                                      al.data_ptr(), be.data_ptr(), bm.data_ptr(), sg.data_ptr(), out.data_ptr(),
+                                      cbuf.data_ptr(), None, _stream()), "cimq_shift_forward")
+    ctx.desc, ctx.sizes = desc, sizes
+    ctx.bufs = (xc, sa_, sw_, al, be, bm, sg, cbuf)
+    ctx.shapes = (wc.shape, alpha.shape if torch.is_tensor(alpha) else al.shape,
+                  beta.shape if torch.is_tensor(beta) else be.shape)
+    return out
+
+
+def _shift_backward(ctx, grad_output):
+    xc, sa, sw, al, be, bm, sg, cbuf = ctx.bufs
+    dev = xc.device
+    wshape, ashape, bshape = ctx.shapes
+    g = grad_output.detach().to(torch.float32).contiguous()
+    gx = torch.empty_like(xc)
+    gw = torch.empty(wshape, device=dev, dtype=torch.float32)
+    ga = torch.empty_like(al)
+    gb = torch.empty_like(be)
+    gsa = torch.empty(1, device=dev, dtype=torch.float32)
+    ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+    lib = _lib.load()
+    _lib.check(lib.cimq_shift_backward(ctx.desc, g.data_ptr(), xc.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+                                       al.data_ptr(), be.data_ptr(), bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(),
+                                       gx.data_ptr(), gw.data_ptr(), ga.data_ptr(), gb.data_ptr(), gsa.data_ptr(),
+                                       ws.data_ptr(), _stream()), "cimq_shift_backward")
+    # full [1, T, nbw, nba, 1, O]: autograd sums them down to a broadcast alpha / beta's own shape
+    return gx, gw, ga, gb, gsa
+
+
+class _ShiftTestFunction:
+    """Shared body of the 14-argument scale + shift Functions of test_backward_cimlayer_scale_
+    shift.py on integer inputs x_int / w_int (no LSQ scales): sa = sw = 1 on the device."""
+
+    @staticmethod
+    def _fwd(ctx, variant, x_int, w_int, conv_stride, conv_padding, conv_dilation, act_bits, act_bit_slice,
+             weight_bits, weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim, beta_cim):
+        if int(weight_bits / weight_bit_slice) != int(act_bits / act_bit_slice):
+            # the reference divides the act-slice grads with the weight-slice count as loop
+            # bound (scale_shift.py:534): only nbw == nba is well defined there
+            raise ValueError("the scale/shift Functions need as many weight as activation bit slices")
+        one = torch.ones(1, device=x_int.device, dtype=torch.float32)
+        zero = torch.zeros(1, device=x_int.device, dtype=torch.float32)
+        ctx.save_for_backward(x_int, w_int)
+        return _shift_forward(ctx, x_int, w_int, one, one, alpha_cim, beta_cim, binary_mask, zero, conv_stride,
+                              conv_padding, conv_dilation, act_bits, act_bit_slice, weight_bits, weight_bit_slice,
+                              adc_bits, arr, variant, _lib.CIMQ_INPUT_XQ, 0.0)
+
+    @staticmethod
+    def _bwd(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018 -- version check of x_int / w_int
+        gx, gw, ga, gb, _ = _shift_backward(ctx, grad_output)
+        return (gx, gw) + (None,) * 10 + (ga, gb)
+
+
+class get_analog_partial_sums_autograd_ver2(torch.autograd.Function):
+    """Scale + shift ADC ``clamp(round((ps-beta)/alpha))*alpha + beta`` on int8-stored partial
+    sums (test_backward_cimlayer_scale_shift.py:336-546): same 14 positional args, grads at 0, 1,
+    12 (alpha_cim) and 13 (beta_cim)."""
+
+    @staticmethod
+    def forward(ctx, x_int, w_int, conv_stride, conv_padding, conv_dilation, act_bits, act_bit_slice,
+                weight_bits, weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim, beta_cim):
+        v = _lib.CIMQ_ADC_SHIFT_ROUND | _lib.CIMQ_ADC_F_PS_INT8 | _lib.CIMQ_ADC_F_SHIFT_RANGE
+        return _ShiftTestFunction._fwd(ctx, v, x_int, w_int, conv_stride, conv_padding, conv_dilation, act_bits,
+                                       act_bit_slice, weight_bits, weight_bit_slice, adc_bits, arr, binary_mask,
+                                       alpha_cim, beta_cim)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return _ShiftTestFunction._bwd(ctx, grad_output)
+
+
+class get_adcless_cim_output(torch.autograd.Function):
+    """Scale + shift sign ADC ``sign((ps-beta)/alpha)*alpha + beta`` (test_backward_cimlayer_scale_
+    shift.py:113-334): same 14 positional args, grads at 0, 1, 12 and 13."""
+
+    @staticmethod
+    def forward(ctx, x_int, w_int, conv_stride, conv_padding, conv_dilation, act_bits, act_bit_slice,
+                weight_bits, weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim, beta_cim):
+        if adc_bits != 1:
+            raise ValueError("get_adcless_cim_output is a 1-bit (sign) ADC")
+        v = _lib.CIMQ_ADC_SHIFT_SIGN | _lib.CIMQ_ADC_F_SHIFT_RANGE
+        return _ShiftTestFunction._fwd(ctx, v, x_int, w_int, conv_stride, conv_padding, conv_dilation, act_bits,
+                                       act_bit_slice, weight_bits, weight_bit_slice, adc_bits, arr, binary_mask,
+                                       alpha_cim, beta_cim)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        return _ShiftTestFunction._bwd(ctx, grad_output)
+
+
+class _CimConv2dLSQShift(torch.autograd.Function):
+    """Conv2dLSQCiM(adc_shift=True): fused act-LSQ + CiM conv whose ADC is the scale + shift one
+    applied to the library's rescaled partial sum u = fp16(ps)*sw*sa (lsq.py:195)."""
+
+    @staticmethod
+    def forward(ctx, x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act, stride, padding, dilation,
+                nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
+        variant = _lib.CIMQ_ADC_SHIFT_SIGN if adcbits == 1 else _lib.CIMQ_ADC_SHIFT_ROUND
+        ctx.save_for_backward(x, w_q)
+        return _shift_forward(ctx, x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act, stride, padding,
+                              dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, variant,
+                              _lib.CIMQ_INPUT_RAW_LSQ, float(2 ** nbits_a - 1))
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018
+        gx, gw, ga, gb, gsa = _shift_backward(ctx, grad_output)
+        return (gx, gw, gsa, None, ga, gb) + (None,) * 11
+
+
+def cim_conv2d_lsq_shift(x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act, stride, padding, dilation,
+                         nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar):
+    """out[B, P, O] of the fused act-LSQ + scale/shift-ADC CiM conv; differentiable in x, w_q, sa,
+    alpha_q and beta.  adcbits 1.5: clamp(round((u-beta)/alpha), -1, 1)*alpha + beta (ver2 on u);
+    adcbits 1: sign((u-beta)/alpha)*alpha + beta (adcless on u)."""
+    if adcbits not in (1, 1.5):
+        raise ValueError("the scale/shift ADC option needs adcbits 1 or 1.5")
+    return _CimConv2dLSQShift.apply(x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act, stride, padding,
+                                    dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar)
 
 
 class _CimModuleConv(torch.autograd.Function):
@@ -182,14 +358,17 @@ class _CimModuleConv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
-                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False):
+                dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False,
+                stochastic=False):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
         qp_a = float(2 ** nbits_a - 1)
         qn_w, qp_w = -(2 ** (nbits_w - 1)), 2 ** (nbits_w - 1) - 1
         desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
-                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a)
+                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a,
+                              _lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
+                              stochastic_seed() if stochastic else 0)
         lsq = _lib.make_lsq_desc(qn_w, qp_w, 1.0 / math.sqrt(x.numel() * qp_a),
                                  1.0 / math.sqrt(weight.numel() * qp_w),
                                  nbits_alpha if alpha_cim is not None else 0)
@@ -263,19 +442,19 @@ class _CimModuleConv(torch.autograd.Function):
                                             None if gac is None else gac.data_ptr(), ws.data_ptr(), _stream()),
                    "cimq_module_backward")
         if targets is not None:
-            return (gx,) + (None,) * 17
-        return (gx, gw, gaa, gaw, gac) + (None,) * 13
+            return (gx,) + (None,) * 18
+        return (gx, gw, gaa, gaw, gac) + (None,) * 14
 
 
 def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                     dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha,
-                    accumulate=False):
+                    accumulate=False, stochastic=False):
     """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
     the three step-size parameters (alpha_act and alpha_weight are 1-element tensors).
-    ``accumulate``: see _CimModuleConv."""
+    ``accumulate``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC."""
     return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
                                 padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
-                                nbits_alpha, accumulate)
+                                nbits_alpha, accumulate, stochastic)
 
 
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,
@@ -306,15 +485,18 @@ def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbi
 
 def debug_partial_sums(x_q, w_q, conv_stride, conv_padding, act_bits, act_bit_slice, weight_bits,
                        weight_bit_slice, adc_bits, arr, binary_mask, alpha_cim, weight_scaling_factor,
-                       act_scaling_factor, signed_act):
+                       act_scaling_factor, signed_act, stochastic=False, seed=None):
     """Forward on the device that also returns the integer partial sums [B,T,nbw,nba,P,O]
     (int32) and the ADC outputs (fp32) -- the reference's ctx.ps_int / adc_out
-    (lsq.py:169-230).  Parity-test hook."""
+    (lsq.py:169-230).  Parity-test hook; ``stochastic`` (with an optional Philox ``seed``)
+    draws the stochastic ADC of lsq.py:205-221."""
     _require_device(x_q)
     dev = x_q.device
     B, C, H, W, O, KH, KW, st, pd = _geometry(x_q, w_q, conv_stride, conv_padding, (1, 1))
     desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, arr, weight_bits, act_bits, weight_bit_slice,
-                          act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ)
+                          act_bit_slice, adc_bits, _lib.CIMQ_INPUT_XQ,
+                          adc_variant=_lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
+                          seed=(stochastic_seed() if seed is None else seed) if stochastic else 0)
     sizes = _lib.query_sizes(desc)
     nbw, nba = int(weight_bits / weight_bit_slice), int(act_bits / act_bit_slice)
     T = int(math.ceil(C * KH * KW / arr))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 3
+#define CIMQ_ABI_VERSION 4
 
 /* status codes */
 #define CIMQ_OK 0
@@ -49,6 +49,22 @@ extern "C" {
 /* what ``x`` holds (cimq_conv_desc.input_kind) */
 #define CIMQ_INPUT_XQ 0     /* x is x_q, the quantised activation handed to the Function (lsq.py:92) */
 #define CIMQ_INPUT_RAW_LSQ 1 /* x is the raw activation; the LSQ act quantiser (lsq.py:547-549) is fused */
+
+/* cimq_conv_desc.adc_variant: which ADC the partial sums go through.  Low byte = variant,
+ * higher bits = CIMQ_ADC_F_* modifiers. */
+#define CIMQ_ADC_LIBRARY 0     /* get_cim_output_signed's ADC (lsq.py:196-230), deterministic */
+#define CIMQ_ADC_STOCHASTIC 1  /* the stochastic 1.5-bit ADC (lsq.py:205-221): 2 x 50 Bernoulli draws
+                                  per partial sum from a Philox4x32-10 stream keyed by seed_lo/hi;
+                                  the backward is the deterministic one (lsq.py:244-386) */
+#define CIMQ_ADC_SHIFT_ROUND 2 /* scale + shift ADC clamp(round((u-beta)/alpha))*alpha + beta
+                                  (test/test_backward_cimlayer_scale_shift.py:336-546, "ver2") */
+#define CIMQ_ADC_SHIFT_SIGN 3  /* scale + shift sign ADC sign((u-beta)/alpha)*alpha + beta
+                                  (test/test_backward_cimlayer_scale_shift.py:113-334, "adcless") */
+#define CIMQ_ADC_F_PS_INT8 0x100     /* partial sums pass through an int8 buffer before the ADC
+                                        (truncation + wrap, scale_shift.py:401) */
+#define CIMQ_ADC_F_SHIFT_RANGE 0x200 /* ADC range Qp = 2^(b-1)-1, Qn = -2^(b-1) for every adc_bits
+                                        but 1 (scale_shift.py:369-375) instead of the library's
+                                        +-1 for 1.5 bits */
 
 /* cimq_lsq_desc.flags */
 #define CIMQ_LSQ_ACCUMULATE_GRADS 1 /* cimq_module_backward adds the parameter gradients into
@@ -65,7 +81,9 @@ typedef struct cimq_conv_desc {
   float adc_bits;     /* 0 (fp ADC), 1 (sign), 1.5 (ternary, alpha scaled), >1.5 (multi-level) */
   int32_t input_kind; /* CIMQ_INPUT_* */
   float lsq_qp;       /* CIMQ_INPUT_RAW_LSQ: act clamp max Qp_a = 2^bits_a - 1 (Qn_a = 0) */
-  int32_t reserved[4];
+  int32_t adc_variant; /* CIMQ_ADC_* | CIMQ_ADC_F_* (0: the library ADC) */
+  uint32_t seed_lo, seed_hi; /* CIMQ_ADC_STOCHASTIC: Philox key of this call */
+  int32_t reserved;
 } cimq_conv_desc;
 
 /* The LSQ quantisers of Conv2dLSQCiM.forward (lsq.py:544-571), for the module entry points. */
@@ -145,6 +163,23 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
 int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
                     const float* sw, const int8_t* binary_mask, const float* signed_act,
                     float* alpha_init, void* ctx, void* ws, void* stream);
+
+/* Forward of the scale + shift CiM conv (adc_variant CIMQ_ADC_SHIFT_ROUND / _SIGN): the
+ * test Functions get_analog_partial_sums_autograd_ver2 / get_adcless_cim_output of
+ * test/test_backward_cimlayer_scale_shift.py (:336-431 / :113-215) when x, w_q are the integer
+ * x_int / w_int with sa = sw = 1, and this build's Conv2dLSQCiM(adc_shift=True) otherwise
+ * (u = fp16(ps) * sw * sa as lsq.py:195 before the shifted ADC).  alpha and beta are
+ * [1, T, nbw, nba, 1, O] fp32; the rest as cimq_forward. */
+int cimq_shift_forward(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,
+                       const float* sw, const float* alpha, const float* beta, const int8_t* binary_mask,
+                       const float* signed_act, float* out, void* ctx, void* ws, void* stream);
+
+/* Backward of cimq_shift_forward (scale_shift.py:437-546 / :240-334): grad_x, grad_w, and
+ * grad_alpha / grad_beta [1, T, nbw, nba, 1, O]; grad_sa as cimq_backward (RAW_LSQ only). */
+int cimq_shift_backward(const cimq_conv_desc* d, const float* grad_out, const float* x, const float* sa,
+                        const float* sw, const float* alpha, const float* beta, const int8_t* binary_mask,
+                        const float* signed_act, const void* ctx, float* grad_x, float* grad_w,
+                        float* grad_alpha, float* grad_beta, float* grad_sa, void* ws, void* stream);
 
 /* Diagnostic / parity hook: cimq_forward that also writes every integer partial sum
  * ps_out[B,T,nbw,nba,P,O] (int32; the reference keeps them as the fp16 ctx.ps_int of

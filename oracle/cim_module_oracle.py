@@ -41,6 +41,25 @@ class OracleCimFunction(torch.autograd.Function):
         return (torch.from_numpy(gx), torch.from_numpy(gw)) + (None,) * 10 + (ga_t,) + (None,) * 4
 
 
+class OracleCimShiftFunction(torch.autograd.Function):
+    """numpy partial-sum Function with the scale/shift ADC option (cim_oracle.adc_apply beta)."""
+
+    @staticmethod
+    def forward(ctx, x_q, w_q, stride, padding, act_bits, act_bs, w_bits, w_bs, adc_bits, arr, binary_mask,
+                alpha_q, beta, sw, sa, signed_act):
+        out, c = co.cim_forward(_np(x_q), _np(w_q), stride, padding, (1, 1), act_bits, act_bs, w_bits, w_bs,
+                                adc_bits, arr, _np(binary_mask), _np(alpha_q), _np(sw), _np(sa), False,
+                                _np(signed_act), beta=_np(beta))
+        ctx.c = c
+        return torch.from_numpy(out)
+
+    @staticmethod
+    def backward(ctx, g):
+        gx, gw, ga, gb = co.cim_backward(ctx.c, _np(g))
+        t = lambda v: torch.from_numpy(np.ascontiguousarray(v))  # noqa: E731
+        return (t(gx), t(gw)) + (None,) * 9 + (t(ga), t(gb)) + (None,) * 3
+
+
 def _gs(x, s):
     """grad_scale (lsq.py:23-26)."""
     yg = x * s
@@ -58,7 +77,7 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
                  groups=1, bias=True, nbits_w=8, nbits_a=8, nbits_alpha=8, wbitslice=1,
-                 abitslice=1, xbar=64, adcbits=6, stochastic_quant=False, **kwargs):
+                 abitslice=1, xbar=64, adcbits=6, stochastic_quant=False, adc_shift=False, **kwargs):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
                          dilation=dilation, groups=groups, bias=bias)
         self.nbits_w, self.nbits_a, self.nbits_alpha = nbits_w, nbits_a, nbits_alpha
@@ -81,6 +100,8 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
         self.register_buffer("signed_act", torch.zeros(1))
         self.register_buffer("init_state_cim", torch.zeros(1))
         self._state_cache = None  # (parity with the product module; unused here)
+        self.adc_shift = bool(adc_shift)
+        self.beta_cim = torch.nn.Parameter(torch.zeros_like(self.alpha_cim)) if self.adc_shift else None
 
     def forward(self, x):
         qn_w, qp_w = co.lsq_weight_params(self.nbits_w)
@@ -115,10 +136,15 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
             alpha_q = _rp(a / scale).clamp(qn_al, qp_al) * scale
         if self.adcbits == 0:
             return F.conv2d(x_q, w_q, self.bias, self.stride, self.padding, self.dilation)
-        out = OracleCimFunction.apply(x_q, w_q, self.stride, self.padding, self.dilation,
-                                      self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice,
-                                      self.adcbits, self.xbar, self.binary_mask, alpha_q, sw, sa,
-                                      self.stochastic_quant, self.signed_act)
+        if self.adc_shift:
+            out = OracleCimShiftFunction.apply(x_q, w_q, self.stride, self.padding, self.nbits_a, self.abitslice,
+                                               self.nbits_w, self.wbitslice, self.adcbits, self.xbar,
+                                               self.binary_mask, alpha_q, self.beta_cim, sw, sa, self.signed_act)
+        else:
+            out = OracleCimFunction.apply(x_q, w_q, self.stride, self.padding, self.dilation,
+                                          self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice,
+                                          self.adcbits, self.xbar, self.binary_mask, alpha_q, sw, sa,
+                                          self.stochastic_quant, self.signed_act)
         fx = int((x_q.shape[-1] - self.weight.shape[-1] + 2 * self.padding[0]) / self.stride[0] + 1)
         out = out.transpose(1, 2).view(x_q.shape[0], self.out_channels, fx, fx)
         if self.bias is not None:

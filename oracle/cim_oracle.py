@@ -212,14 +212,25 @@ def _tiles(K: int, arr: int):
     return t
 
 
-def adc_apply(ps16, adc_bits, alpha_cim, sw, sa):
-    """u = ps*sw*sa (lsq.py:195) and the ADC of lsq.py:197-230 on fp16 partial sums."""
+def adc_apply(ps16, adc_bits, alpha_cim, sw, sa, beta=None):
+    """u = ps*sw*sa (lsq.py:195) and the ADC of lsq.py:197-230 on fp16 partial sums.
+
+    ``beta`` (this build's scale/shift module option, not in the reference library): the
+    shifted ADC of test/test_backward_cimlayer_scale_shift.py applied to u -- adc 1.5:
+    ``clamp(round((u-beta)/alpha), -1, 1)*alpha + beta`` (ver2, :421-425); adc 1:
+    ``sign((u-beta)/alpha)*alpha + beta`` (adcless, :202-211)."""
     qn, qp = adc_range(adc_bits)
     sa = np.asarray(sa, F32).reshape(1)
     sw = np.asarray(sw, F32).reshape(1)
     u = ((np.asarray(ps16).astype(F32) * sw).astype(F32) * sa).astype(F32)
     with np.errstate(all="ignore"):
-        if adc_bits == 0:                                            # :197
+        if beta is not None:
+            a = np.asarray(alpha_cim, F32)
+            b = np.asarray(beta, F32)
+            v = ((u - b).astype(F32) / a).astype(F32)
+            code = np.sign(v) if adc_bits == 1 else np.clip(np.rint(v), F32(qn), F32(qp))
+            adc = ((code.astype(F32) * a).astype(F32) + b).astype(F32)
+        elif adc_bits == 0:                                          # :197
             adc = u
         elif adc_bits == 1:                                          # :200
             adc = (np.sign(u) * np.asarray(alpha_cim, F32)).astype(F32)
@@ -240,11 +251,14 @@ class CimCtx:
 
 def cim_forward(x_q, w_q, stride, padding, dilation, act_bits, act_bs, w_bits, w_bs,
                 adc_bits, arr, binary_mask, alpha_cim, sw, sa, stochastic=False,
-                signed_act=0.0, return_debug=False):
+                signed_act=0.0, return_debug=False, beta=None):
     """``get_cim_output_signed.forward`` (lsq.py:92-237). Returns out [B, P, O] fp32
-    and the saved context (int8 x_int, int8 weight slices, fp16 partial sums)."""
+    and the saved context (int8 x_int, int8 weight slices, fp16 partial sums).
+    ``beta``: the scale/shift module option (adc_apply)."""
     if stochastic:
-        raise NotImplementedError("stochastic ADC is statistical; no bit-exact oracle")
+        raise NotImplementedError("stochastic ADC is statistical; see stochastic_adc_expectation")
+    if beta is not None and adc_bits not in (1, 1.5):
+        raise ValueError("the scale/shift ADC option needs adc_bits 1 or 1.5")
     x_q = np.asarray(x_q, F32)
     w_q = np.asarray(w_q, F32)
     sa = np.asarray(sa, F32).reshape(1)
@@ -275,13 +289,14 @@ def cim_forward(x_q, w_q, stride, padding, dilation, act_bits, act_bs, w_bits, w
             for kk in range(nbw):
                 ps[:, i, kk, j] = np.matmul(xs[:, j, :, lo:hi], ws[kk, lo:hi, :]).astype(F16)
     ctx.ps16 = ps                                                    # :192
-    u, adc = adc_apply(ps, adc_bits, alpha_cim, sw, sa)
+    u, adc = adc_apply(ps, adc_bits, alpha_cim, sw, sa, beta)
     out = np.sum((adc * binary_mask.astype(F32)).astype(F32), axis=(1, 2, 3), dtype=F32)  # :233
     ctx.meta = dict(stride=tuple(stride), padding=tuple(padding), k=k, C=C, O=O, H=x_q.shape[2],
                     W=x_q.shape[3], nbw=nbw, nba=nba, w_bs=w_bs, act_bs=act_bs, act_bits=act_bits,
                     adc_bits=adc_bits, arr=arr, T=T, K=K, P=P, B=B, qn=qn, qp=qp)
     ctx.sw, ctx.sa = sw, sa
     ctx.alpha = None if alpha_cim is None else np.asarray(alpha_cim, F32)
+    ctx.beta = None if beta is None else np.asarray(beta, F32)
     ctx.binary_mask = binary_mask
     ctx.signed_act = float(np.asarray(signed_act).reshape(-1)[0])
     if return_debug:
@@ -292,7 +307,8 @@ def cim_forward(x_q, w_q, stride, padding, dilation, act_bits, act_bs, w_bits, w
 def cim_backward(ctx: CimCtx, grad_out: np.ndarray, absolute: bool = False):
     """``get_cim_output_signed.backward`` (lsq.py:244-386).
 
-    Returns (grad_x [B,C,H,W], grad_w [O,C,k,k], grad_alpha [1,T,nbw,nba,1,O] or None).
+    Returns (grad_x [B,C,H,W], grad_w [O,C,k,k], grad_alpha [1,T,nbw,nba,1,O] or None);
+    with the scale/shift option (ctx.beta) also grad_beta as a fourth element.
     ``absolute=True`` re-runs the same contraction in fp64 on |operands|, giving the
     per-element sum of |terms| that the parity tolerances are scaled by."""
     m = ctx.meta
@@ -307,6 +323,8 @@ def cim_backward(ctx: CimCtx, grad_out: np.ndarray, absolute: bool = False):
         # the clamp masks and ADC codes are decided in fp32 even for the |terms| pass
         if adc_bits in (1, 1.5):                                     # :257-264
             ps = ((ctx.ps16.astype(F32) * ctx.sw).astype(F32) * ctx.sa).astype(F32)
+            if ctx.beta is not None:  # scale/shift option: shifted like the ADC input
+                ps = (ps - ctx.beta).astype(F32)
             ps = (ps / ctx.alpha).astype(F32)
         else:
             ps = ctx.ps16.astype(F32)
@@ -325,13 +343,26 @@ def cim_backward(ctx: CimCtx, grad_out: np.ndarray, absolute: bool = False):
     greater = ps >= thr_hi                                                       # :310
     lesser = ps <= thr_lo                                                        # :311
     Gm = np.where(greater | lesser, dt(0), G).astype(dt)                         # :313
-    grad_alpha = None
+    grad_alpha = grad_beta = None
     numel = ps.size
     c = F32(1.0 / math.sqrt(numel * m["qp"])) if adc_bits in (1, 1.5) else None
-    if adc_bits == 1:                                                            # :321-325
+    if adc_bits == 1 and ctx.beta is None:                                       # :321-325
         q = np.sign(ps).astype(dt)
         terms = ((A(q) * c).astype(dt) * A(G_after)).astype(dt)
         grad_alpha = np.sum(terms, axis=(0, 4), keepdims=True)
+    if ctx.beta is not None:  # scale/shift option (test_backward_cimlayer_scale_shift.py)
+        clamped = greater | lesser
+        if adc_bits == 1.5:                                                      # ver2 :488-501
+            with np.errstate(invalid="ignore"):
+                q = (np.rint(ps) - ps).astype(F32).astype(dt)
+            q = np.where(greater, dt(m["qp"]), q)
+            q = np.where(lesser, dt(m["qn"]), q)
+            grad_alpha = np.sum((A(q) * A(G_after)).astype(dt), axis=(0, 4), keepdims=True)
+            grad_beta = np.sum(np.where(clamped, A(G_after), dt(0)), axis=(0, 4), keepdims=True)
+        else:                                                                    # adcless :281-287
+            terms = ((A(np.sign(ps).astype(dt)) * c).astype(dt) * A(G_after)).astype(dt)
+            grad_alpha = np.sum(terms, axis=(0, 4), keepdims=True)
+            grad_beta = np.sum(A(G_after), axis=(0, 4), keepdims=True)
     elif adc_bits == 1.5:                                                        # :326-332
         q = np.rint(ps).astype(dt)
         q = np.where(greater, dt(m["qp"]), q)
@@ -358,7 +389,10 @@ def cim_backward(ctx: CimCtx, grad_out: np.ndarray, absolute: bool = False):
         gi[:, i] = gi[:, i] / dt((2 ** m["act_bs"]) ** i)
     gi = gi.mean(axis=1, dtype=dt).astype(dt)                                    # :376
     gx = fold(gi.transpose(0, 2, 1), (m["H"], m["W"]), k, m["padding"], m["stride"])  # :380-382
-    return gx.astype(dt), gw.astype(dt), (None if grad_alpha is None else grad_alpha.astype(dt))
+    ga = None if grad_alpha is None else grad_alpha.astype(dt)
+    if ctx.beta is not None:
+        return gx.astype(dt), gw.astype(dt), ga, grad_beta.astype(dt)
+    return gx.astype(dt), gw.astype(dt), ga
 
 
 # ----------------------------------------------------------------------------------------
@@ -394,3 +428,44 @@ def alpha_cim_init(x_q, w_q, stride, padding, act_bits, act_bs, w_bits, w_bs, ar
     t = (t / F32(math.sqrt(qp))).astype(F32)
     fill = (np.asarray(sw, F32).reshape(1) * F32(1.0)).astype(F32) * np.asarray(sa, F32).reshape(1)
     return np.where(t == 0, fill.astype(F32), t).astype(F32)
+
+
+# ----------------------------------------------------------------------------------------
+# stochastic 1.5-bit ADC (lsq.py:205-221): exact code distribution per partial sum
+# ----------------------------------------------------------------------------------------
+def _binom_pmf(n: int, p: np.ndarray) -> np.ndarray:
+    """[..., n+1] probabilities of Binomial(n, p) (float64)."""
+    p = np.asarray(p, np.float64)[..., None]
+    k = np.arange(n + 1, dtype=np.float64)
+    logc = np.array([math.lgamma(n + 1) - math.lgamma(i + 1) - math.lgamma(n - i + 1) for i in range(n + 1)])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lp = logc + k * np.log(p) + (n - k) * np.log1p(-p)
+    pmf = np.exp(lp)
+    pmf = np.where(p <= 0, (k == 0).astype(np.float64), pmf)
+    pmf = np.where(p >= 1, (k == n).astype(np.float64), pmf)
+    return pmf
+
+
+def stochastic_code_probs(u: np.ndarray, alpha: np.ndarray, num_iter: int = 50, sharpness: float = 0.01):
+    """P(code = +1), P(code = -1) of the stochastic ADC for rescaled partial sums u.
+
+    s1 = sigmoid((u - alpha/2)/0.01), s2 = sigmoid((u + alpha/2)/0.01) (lsq.py:210-211);
+    n_i ~ Binomial(50, s_i) (the sums of ceil(s_i - U), :214-217); code =
+    clamp(round(n1/50 + n2/50 - 1), -1, 1) evaluated in fp32 as torch does (:219-220)."""
+    u = np.asarray(u, F32)
+    a = np.asarray(alpha, F32)
+    h = (F32(0.5) * a).astype(F32)
+    z1 = ((u - h).astype(F32) / F32(sharpness)).astype(F32)
+    z2 = ((u + h).astype(F32) / F32(sharpness)).astype(F32)
+    with np.errstate(over="ignore"):
+        s1 = (F32(1) / (F32(1) + np.exp(-z1))).astype(F32)
+        s2 = (F32(1) / (F32(1) + np.exp(-z2))).astype(F32)
+    n = np.arange(num_iter + 1, dtype=F32)
+    fr = (n / F32(num_iter)).astype(F32)
+    v = ((fr[:, None] + fr[None, :]).astype(F32) - F32(1)).astype(F32)  # [n1, n2]
+    code = np.clip(np.rint(v), -1, 1)
+    p1 = _binom_pmf(num_iter, s1)
+    p2 = _binom_pmf(num_iter, s2)
+    plus = np.einsum("...i,ij,...j->...", p1, (code == 1).astype(np.float64), p2)
+    minus = np.einsum("...i,ij,...j->...", p1, (code == -1).astype(np.float64), p2)
+    return plus, minus

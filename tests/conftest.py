@@ -54,3 +54,8 @@ def cuda_device():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     return torch.device("cuda:0")
+
+
+def shift_manifest():
+    with open(os.path.join(GOLDEN, "manifest_shift.json")) as f:
+        return json.load(f)
