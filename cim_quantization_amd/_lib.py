@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "cimq_shift_forward",
     "cimq_shift_backward",
     "cimq_debug_partial_sums",
+    "cimq_debug_state_codes",
     "cimq_profile_start",
     "cimq_profile_stop",
 )
@@ -119,6 +120,8 @@ def _bind(lib):
     lib.cimq_shift_backward.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 16
     lib.cimq_debug_partial_sums.restype = ctypes.c_int
     lib.cimq_debug_partial_sums.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
+    lib.cimq_debug_state_codes.restype = ctypes.c_int
+    lib.cimq_debug_state_codes.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 4
     lib.cimq_profile_start.restype = ctypes.c_int
     lib.cimq_profile_start.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.cimq_profile_stop.restype = ctypes.c_int

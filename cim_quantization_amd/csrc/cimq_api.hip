@@ -204,6 +204,20 @@ int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float
   return launch_fwd_any(g, c, sw, sa, out, ps_out, adc_out, s);
 }
 
+int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* code_out, uint8_t* pass_out,
+                           void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!ctx || !code_out || !pass_out) return fail(CIMQ_EINVAL, "null pointer argument");
+  if (!v7_plan(g).ok) return fail(CIMQ_EUNSUPPORTED, "this layer's forward writes no v7 state words");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  const long long n = (long long)g.T * g.M * g.O;
+  hipLaunchKernelGGL(decode_state_kernel, dim3(std::min(cdiv(n, 256), 8192)), dim3(256), 0, s, g, g.NBP == 8 ? 1 : 0,
+                     c + ctx_layout(g).st, code_out, pass_out);
+  return check_hip("decode_state");
+}
+
 int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x, const float* sa,
                   const float* sw, const float* alpha_q, const int8_t* binary_mask,
                   const float* signed_act, const void* ctx, float* grad_x, float* grad_w,

@@ -344,6 +344,42 @@ __global__ __launch_bounds__(1024) void module_bwd_finish_kernel(LsqArgs q, Modu
 }
 
 // layout changes for the general (non-fast-path) kernels in module mode
+// Parity hook: the ADC code and STE-pass bit of every partial sum, decoded from the state
+// words cim_fwd_v3_kernel<.., CST> wrote (compact: bits 3*(k*nba + j) + {0 pass, 1 code != 0,
+// 2 code < 0} of st32[(i*M + m)*O + o]; planes: bit k*nba + j of st64[((i*M + m)*O + o)*3 + q]),
+// in the reference's [B, T, nbw, nba, P, O] order.
+__global__ void decode_state_kernel(Geo g, int planes, const uint8_t* __restrict__ st, int8_t* __restrict__ code,
+                                    uint8_t* __restrict__ pass) {
+  const size_t n = (size_t)g.T * g.M * g.O;
+  const int nkj = g.nbw * g.nba;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const int o = (int)(e % g.O);
+    const size_t im = e / g.O;
+    const int m = (int)(im % g.M), i = (int)(im / g.M);
+    const int b = m / g.P, p = m - b * g.P;
+    uint64_t ps = 0, nz = 0, ng = 0;
+    uint32_t w32 = 0;
+    if (planes) {
+      const uint64_t* s64 = reinterpret_cast<const uint64_t*>(st) + e * 3;
+      ps = s64[0]; nz = s64[1]; ng = s64[2];
+    } else {
+      w32 = reinterpret_cast<const uint32_t*>(st)[e];
+    }
+    for (int kj = 0; kj < nkj; ++kj) {
+      const int k = kj / g.nba, j = kj - k * g.nba;
+      int bp, bz, bn;
+      if (planes) {
+        bp = (int)((ps >> kj) & 1u); bz = (int)((nz >> kj) & 1u); bn = (int)((ng >> kj) & 1u);
+      } else {
+        bp = (w32 >> (3 * kj)) & 1; bz = (w32 >> (3 * kj + 1)) & 1; bn = (w32 >> (3 * kj + 2)) & 1;
+      }
+      const size_t di = ((((size_t)b * g.T + i) * g.nbw + k) * g.nba + j) * g.P * g.O + (size_t)p * g.O + o;
+      code[di] = (int8_t)(bz ? (bn ? -1 : 1) : 0);
+      pass[di] = (uint8_t)bp;
+    }
+  }
+}
+
 __global__ void bpo_to_nchw_kernel(Geo g, const float* __restrict__ src, float* __restrict__ dst) {
   const size_t n = (size_t)g.M * g.O;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {

@@ -521,6 +521,30 @@ def debug_partial_sums(x_q, w_q, conv_stride, conv_padding, act_bits, act_bit_sl
     return out, ps, adc
 
 
+def debug_state_codes(out):
+    """ADC codes (int8) and STE-pass bits (uint8) [B, T, nbw, nba, P, O] of every partial sum that
+    the production forward (cim_fwd_v3_kernel, v7 path) recorded for ``out`` -- the output of
+    get_cim_output_signed / cim_conv2d_lsq / cim_module_conv whose backward has not run yet.
+    Parity-test hook (cimq_debug_state_codes)."""
+    ctx = out.grad_fn
+    while ctx is not None and not hasattr(ctx, "desc"):  # through views (the module's NCHW reshape)
+        ctx = ctx.next_functions[0][0] if ctx.next_functions else None
+    if ctx is None:
+        raise RuntimeError("no libcimq forward context behind this tensor")
+    d = ctx.desc
+    cbuf = ctx.bufs[-1]
+    nbw, nba = int(d.bits_w / d.bs_w), int(d.bits_a / d.bs_a)
+    T = num_xbars(d.in_channels, (d.kernel_h, d.kernel_w), d.xbar)
+    Ho = (d.in_h + 2 * d.pad_h - d.kernel_h) // d.stride_h + 1
+    Wo = (d.in_w + 2 * d.pad_w - d.kernel_w) // d.stride_w + 1
+    shape = (d.batch, T, nbw, nba, Ho * Wo, d.out_channels)
+    code = torch.empty(shape, device=cbuf.device, dtype=torch.int8)
+    passed = torch.empty(shape, device=cbuf.device, dtype=torch.uint8)
+    _lib.check(_lib.load().cimq_debug_state_codes(d, cbuf.data_ptr(), code.data_ptr(), passed.data_ptr(), _stream()),
+               "cimq_debug_state_codes")
+    return code, passed
+
+
 def logical_macs(B, C, H, W, O, KH, KW, stride, padding) -> int:
     """ptflops convention B*Ho*Wo*O*C*KH*KW (utils/ptflops/flops_counter.py:314-318)."""
     Ho = (H + 2 * padding[0] - KH) // stride[0] + 1

@@ -190,6 +190,15 @@ int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float
                             const float* signed_act, float* out, int32_t* ps_out, float* adc_out,
                             void* ctx, void* stream);
 
+/* Parity hook for the production forward: decodes the per-partial-sum state words that the
+ * fast forward (cim_fwd_v3_kernel on the v7 path) left in ``ctx`` -- the ADC code
+ * (lsq.py:321-332: -1 / 0 / +1) and the STE pass bit (lsq.py:310-313) of every (tile, w-slice,
+ * a-slice) partial sum -- into code_out / pass_out [B, T, nbw, nba, P, O] (int8 / uint8).
+ * ``ctx`` must come from cimq_forward / cimq_module_forward with the same descriptor;
+ * CIMQ_EUNSUPPORTED for layers whose forward writes no state words. */
+int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* code_out, uint8_t* pass_out,
+                           void* stream);
+
 /* Diagnostic kernel timer.  Until cimq_profile_stop(), every launch of kernel ``kernel_id``
  * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep, each over
  * all kernel variants; 5 / 6 / 7 = only the v7-path forward / grad_x / grad_w kernels) is
