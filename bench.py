@@ -224,36 +224,76 @@ def layer_breakdown(trainer, xs, gs, dev):
 
 
 def cpu_baseline(batch_cpu: int, threads: int):
-    """The numpy oracle (a faithful port of the reference's CPU op sequence) timed on the host:
-    forward + backward of all 19 CiM convs at a bounded batch."""
+    """The op-faithful torch-CPU port of the reference's Function (oracle/cim_torch_port.py: the
+    lsq.py:92-386 op sequence, bit-identical to the reference and 0.95-0.98x its time in the
+    build container, tools/cpu_port_ratio.py) timed on this box's host cores: forward + backward
+    of all 19 ResNet-20 CiM convs at ``batch_cpu`` (default: the full batch 256)."""
     import numpy as np
-    from threadpoolctl import threadpool_limits
 
     from oracle import cim_oracle as co
+    from oracle import cim_torch_port as tp
+    torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
-    with threadpool_limits(limits=threads):
-        t = 0.0
-        for name, c, o, h, s, nb in RESNET20:
-            sa = np.array([0.11], np.float32)
-            sw = np.array([0.07], np.float32)
-            qn_w, qp_w = co.lsq_weight_params(nb)
-            x_q = (rng.integers(0, 2 ** nb, (batch_cpu, c, h, h)).astype(np.float32) * sa).astype(np.float32)
-            w_q = (rng.integers(qn_w, qp_w + 1, (o, c, 3, 3)).astype(np.float32) * sw).astype(np.float32)
-            T = math.ceil(c * 9 / XBAR)
-            a = (rng.random((1, T, nb, nb, 1, o)).astype(np.float32) * 3 + 0.1) * np.float32(sa[0] * sw[0])
-            aq = co.alpha_quantize(a.astype(np.float32), 8)
-            bm = co.make_binary_mask(nb, nb, 1, 1)
-            ho = out_hw(h, s)
-            g = rng.standard_normal((batch_cpu, ho * ho, o)).astype(np.float32)
-            t0 = time.perf_counter()
-            _, ctx = co.cim_forward(x_q, w_q, (s, s), (1, 1), (1, 1), nb, 1, nb, 1, ADC, XBAR, bm, aq, sw, sa,
-                                    False, np.zeros(1, np.float32))
-            co.cim_backward(ctx, g)
-            t += time.perf_counter() - t0
+    t = 0.0
+    for name, c, o, h, s, nb in RESNET20:
+        sa = torch.tensor([0.11])
+        sw = torch.tensor([0.07])
+        qn_w, qp_w = co.lsq_weight_params(nb)
+        x_q = torch.from_numpy(rng.integers(0, 2 ** nb, (batch_cpu, c, h, h)).astype(np.float32)) * sa
+        w_q = torch.from_numpy(rng.integers(qn_w, qp_w + 1, (o, c, 3, 3)).astype(np.float32)) * sw
+        T = math.ceil(c * 9 / XBAR)
+        a = torch.from_numpy(co.alpha_quantize(((rng.random((1, T, nb, nb, 1, o)) * 3 + 0.1) * 0.11 * 0.07)
+                                               .astype(np.float32), 8))
+        bm = torch.from_numpy(co.make_binary_mask(nb, nb, 1, 1))
+        ho = out_hw(h, s)
+        g = torch.from_numpy(rng.standard_normal((batch_cpu, ho * ho, o)).astype(np.float32))
+        t0 = time.perf_counter()
+        out, ctx = tp.cim_forward(x_q, w_q, (s, s), (1, 1), nb, 1, nb, 1, ADC, XBAR, bm, a, sw, sa,
+                                  signed_act=(name == "conv1"))
+        tp.cim_backward(ctx, g)
+        t += time.perf_counter() - t0
     macs = macs_per_sample() * batch_cpu
-    return dict(value=macs / t, unit="MAC/s", cores=threads, kind="port",
-                sample=f"numpy oracle fwd+bwd of the 19 ResNet-20 CiM convs at batch {batch_cpu} "
-                       f"({t:.2f} s, {threads} BLAS threads; elementwise single-threaded)")
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return dict(value=macs / t, unit="MAC/s", cores=threads, kind="port", seconds=t, cpu=cpu,
+                sample=f"op-faithful torch-CPU port of get_cim_output_signed (oracle/cim_torch_port.py), fwd+bwd "
+                       f"of the 19 ResNet-20 CiM convs at batch {batch_cpu}, {threads} threads, {t:.2f} s",
+                reference_in_container={"resnet20_b256_fwd_bwd_s": 27.99, "threads": 8,
+                                        "source": "SURVEY.md section 6 (whole model incl. BN/FC, 8 Xeon cores)",
+                                        "port_over_reference_time": [0.952, 0.981],
+                                        "ratio_source": "tools/cpu_port_ratio.py, layer1 / layer3 at B=256"})
+
+
+def bench_cfg5(dev, steps, warmup):
+    """BASELINE cfg5: QuantLinear 1024->1024 w4a4, 128-row tiles, batch 4096, as Conv2dLSQCiM(k=1)
+     through the module path: fwd+bwd ms per step and forward MAC/s."""
+    import cim_quantization_amd._modules as my_nn
+    torch.manual_seed(7)
+    m = my_nn.Conv2dLSQCiM(1024, 1024, 1, 1, 0, bias=False, nbits_w=4, nbits_a=4, nbits_alpha=8, wbitslice=1,
+                           abitslice=1, xbar=128, adcbits=1.5).to(dev).train()
+    x = torch.randn(4096, 1024, 1, 1, device=dev).relu()
+    gy = torch.randn(4096, 1024, 1, 1, device=dev) / 2048.0
+    for _ in range(max(1, warmup)):
+        m(x).backward(gy)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m(x).backward(gy)
+    torch.cuda.synchronize(dev)
+    fb = (time.perf_counter() - t0) / steps
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m(x)
+        torch.cuda.synchronize(dev)
+    fw = (time.perf_counter() - t0) / steps
+    macs = 4096 * 1024 * 1024
+    return {"workload": "quantlinear_1024x1024_w4a4_xbar128_b4096", "ms_fwd_bwd": fb * 1e3, "ms_fwd": fw * 1e3,
+            "fwd_mac_per_s": macs / fw, "fwd_bwd_mac_per_s": macs / fb, "launch": "eager"}
 
 
 def main():
@@ -262,7 +302,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--cpu-batch", type=int, default=12)
+    ap.add_argument("--cpu-batch", type=int, default=256)
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE cfg5 (QuantLinear) extra line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from the host each step")
     args = ap.parse_args()
@@ -367,6 +408,8 @@ def main():
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
     }
+    if world == 1 and not args.no_cfg5:
+        result["extra_configs"] = {"cfg5": bench_cfg5(dev, args.steps, args.warmup)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_batch, min(16, os.cpu_count() or 1))
     if rank == 0:

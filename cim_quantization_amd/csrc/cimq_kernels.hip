@@ -739,11 +739,14 @@ __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __
     mend = min(mbeg + 64, g.M);
   }
 
+  // global-accumulator blocks own one crossbar tile each (blockIdx.y): the tiles' f ranges are
+  // disjoint, so the grid has T times more blocks for the same work
+  const int i_lo = LDS_ACC ? 0 : (int)blockIdx.y, i_hi = LDS_ACC ? g.T : (int)blockIdx.y + 1;
   for (int m0 = mbeg; m0 < mend; m0 += 64) {
     __syncthreads();
     build_rowinfo(g, m0, sm.rowinfo);
     if (LDS_ACC && threadIdx.x < 64 && m0 + (int)threadIdx.x >= mend) sm.rowinfo[threadIdx.x].w = 0;
-    for (int i = 0; i < g.T; ++i) {
+    for (int i = i_lo; i < i_hi; ++i) {
       __syncthreads();
       build_ftable(g, i, sm.foff, sm.fkk);
       __syncthreads();

@@ -87,7 +87,7 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     return check_hip("cim_bwd_gx_v5");
   }
   const int8_t* xc = reinterpret_cast<const int8_t*>(ctx + L.xcode);
-  if (gx_lds_ok(g)) {
+  if (gx_lds_ok(g) && g.P >= 64) {  // one block per image: only when an image fills a 64-pixel tile
     const size_t lds = lds_tile(g) + sizeof(float) * g.C * g.HW;
     auto kern = cim_bwd_gx_kernel<NBP, FBMAX, true>;
     CIMQ_TRY(set_lds(kern, lds));
@@ -101,7 +101,7 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
   auto kern = cim_bwd_gx_kernel<NBP, FBMAX, false>;
   CIMQ_TRY(set_lds(kern, lds));
   const int slot = prof_begin(KID_BWD_GX, g, s);
-  hipLaunchKernelGGL(kern, dim3(cdiv(g.M, 64)), dim3(256), lds, s, g, xc, wf, wg, pp, sw, sa, gout, gx);
+  hipLaunchKernelGGL(kern, dim3(cdiv(g.M, 64), g.T), dim3(256), lds, s, g, xc, wf, wg, pp, sw, sa, gout, gx);
   prof_end(slot, s);
   CIMQ_TRY(check_hip("cim_bwd_gx(global)"));
   int grid = cdiv(g.Nin, 256);
