@@ -370,6 +370,10 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #endif
   zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * v.RH * v.WP * NBP / 4);
 
+  __syncthreads();
+  // w8a8: is binary_mask the standard int8-wrapped one (zero exactly where j + k >= 8)?
+  const bool std8 = CST != 8 ||
+                    __builtin_amdgcn_ballot_w64(lane < nkj && ((ckl[lane < nkj ? lane : 0] != 0.f) != ((lane >> 3) + (lane & 7) < 8))) == 0ull;
   const int pl = wave * 16 + r16;  // this lane's gather pixel within the m-tile
   const int rb = ((pl >> v.lw) * g.SH) * v.WP + (pl & (Wo - 1)) * g.SW;
   const int tiles_per_img = g.P >> 6;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #ifdef CIMQ_EXP_FWD_NOGATHER
       for (int a = 0; a < NBP; ++a) for (int c = 0; c < KS; ++c) xs[a][c] = v4i{lane, a, c, i};
 #else
-      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, (CST > 0 && !literal) ? KS : ksn);
+      gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, (CST > 0 && !literal && std8) ? KS : ksn);
 #endif
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
@@ -419,11 +423,16 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       for (int a = 0; a < OBM; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c) pl[a][c][0] = pl[a][c][1] = pl[a][c][2] = 0ull;
-      if (CST > 0 && !literal) {
+      if (CST > 0 && !literal && std8) {
         // fast path: slice pairs kj = k*CST + j in descending order, so that shifting each
         // state bit in from the bottom leaves bit 3*kj + {0,1,2} (interleaved words) or bit
-        // kj of each 64-bit plane (PLF) where cimq_v7.hip reads it
+        // kj of each 64-bit plane (PLF) where cimq_v7.hip reads it.  w8a8 (CST 8) runs it only
+        // with the standard int8-wrapped binary_mask (_quan_base.py:207-214), whose pairs with
+        // j + k >= 8 are 0: they add adc * 0 = 0 to the output and G * 0 = 0 to every gradient,
+        // so neither their MFMAs nor their ADC run and their state bits stay 0 (exact: this path
+        // has finite ADC outputs).  Any other mask takes the per-pair loop below.
         constexpr int NS = CST > 0 ? CST : 1;
+
         uint32_t sw3[OBM][4][PLF ? 6 : 1];
 #pragma unroll
         for (int a = 0; a < OBM; ++a)
@@ -443,15 +452,31 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #pragma unroll
               for (int j = 0; j < NS; ++j) {
                 ps[j] = v4i{0, 0, 0, 0};
+                if (CST != 8 || j + k < 8) {  // compile time once unrolled (w8a8: standard mask only)
 #pragma unroll
-                for (int ks = 0; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+                  for (int ks = 0; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+                }
               }
 #pragma unroll
               for (int j = NS - 1; j >= 0; --j) {
+                const int kj = k * NS + j;
+                if (CST == 8 && j + k >= 8) {  // mask-0 pair of the wrapped 8-bit mask: zero state bits
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    if constexpr (PLF) {
+                      const int wd = kj >= 32 ? 1 : 0;
+                      sw3[ob][r][wd] <<= 1;
+                      sw3[ob][r][2 + wd] <<= 1;
+                      sw3[ob][r][4 + wd] <<= 1;
+                    } else {
+                      sw3[ob][r][0] <<= 3;
+                    }
+                  }
+                  continue;
+                }
                 const int pcol = (j * NS + k) * NOB * 16 + ob * 16 + r16;
                 const int4 pv = pt[pcol];
                 const float cf = ct[pcol];
-                const int kj = k * NS + j;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
 #ifdef CIMQ_EXP_FWD_NOADC
@@ -489,7 +514,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
             }
           }
       }
-      for (int k = 0; k < ((CST > 0 && !literal) ? 0 : g.nbw); ++k) {
+      for (int k = 0; k < ((CST > 0 && !literal && std8) ? 0 : g.nbw); ++k) {
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
           if (ob < nob) {

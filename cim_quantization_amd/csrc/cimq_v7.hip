@@ -68,6 +68,13 @@ __host__ __device__ constexpr uint32_t pass_mask_j(int j, int nbw, int nba) {
   return m;
 }
 
+// uniform (scalar-register) copies of values every lane computed identically
+__device__ inline float sgpr_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ inline uint64_t sgpr_u64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+
 // lane l <- lane l+1 / l-1 of the same 16-lane row (0 past the row's end)
 __device__ inline float dpp_from_next(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, true));
@@ -123,15 +130,33 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
   const int Wo = 1 << v.lw;
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cel[t] = pp.ckj[NKJ + t];
   __syncthreads();
-  // nominal binary mask: cE_kj independent of j, so E_k = cE_k0 * popcount(pass bits of k)
+  // two-level binary mask: per slice k, every cE_kj is 0, v1_k or v2_k, so that
+  // E_k = v1_k * popcount(pass bits in M1_k) + v2_k * popcount(pass bits in M2_k).  The plain
+  // mask has one level (cE_kj = 2^(bsw*k) for every j); the int8-wrapped 8-bit mask two
+  // (2^k, and -2^k at j + k = 7) plus zeros (j + k >= 8).  Bits are in state-word coordinates.
   bool nominal = true;
-  float cek[NBW];
+  float ev1[NBW], ev2[NBW];
+  uint64_t em1[NBW], em2[NBW];
 #pragma unroll
   for (int k = 0; k < NBW; ++k) {
-    cek[k] = cel[k * NBA];
+    float v1 = 0.f, v2 = 0.f;
+    uint64_t m1 = 0ull, m2 = 0ull;
 #pragma unroll
-    for (int j = 1; j < NBA; ++j) nominal = nominal && (cel[k * NBA + j] == cek[k]);
+    for (int j = 0; j < NBA; ++j) {
+      const float c = cel[k * NBA + j];
+      const uint64_t bit = PLS ? (1ull << (k * NBA + j)) : (1ull << (3 * (k * NBA + j)));
+      if (c == 0.f) continue;
+      if (m1 == 0ull || c == v1) { v1 = c; m1 |= bit; }
+      else if (m2 == 0ull || c == v2) { v2 = c; m2 |= bit; }
+      else nominal = false;
+    }
+    ev1[k] = sgpr_f(v1); ev2[k] = sgpr_f(v2); em1[k] = sgpr_u64(m1); em2[k] = sgpr_u64(m2);
   }
+  // interleaved words (<= 10 pairs): the plain one-level mask takes the compile-time pass masks,
+  // anything else the per-pair sum; plane words (w8a8) use the two-level form
+  bool single = nominal && !PLS;
+#pragma unroll
+  for (int k = 0; k < NBW; ++k) single = single && em2[k] == 0ull && em1[k] == (uint64_t)pass_mask_k(k, NBA);
   const float scale = sw / (float)NBA;
   float gpart = 0.f;
   int done = r0 - 1;
@@ -190,14 +215,15 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
             if constexpr (PLS) {
               const uint32_t fld = (uint32_t)(sp[ob][r] >> (k * NBA)) & ((1u << NBA) - 1u);
               if (nominal) {
-                E = cek[k] * (float)__popc(fld);
+                E = ev1[k] * (float)__popcll(sp[ob][r] & em1[k]);
+                if (em2[k]) E += ev2[k] * (float)__popcll(sp[ob][r] & em2[k]);
               } else {
                 E = 0.f;
 #pragma unroll
                 for (int j = 0; j < NBA; ++j) E += ((fld >> j) & 1u) ? cel[k * NBA + j] : 0.f;
               }
-            } else if (nominal) {
-              E = cek[k] * (float)__popc(sv[ob][r] & pass_mask_k(k, NBA));
+            } else if (single) {
+              E = ev1[k] * (float)__popc(sv[ob][r] & pass_mask_k(k, NBA));
             } else {
               E = 0.f;
 #pragma unroll
@@ -410,15 +436,31 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   float* red = reinterpret_cast<float*>(cur);  // [4 waves][NTL][NKJ][16] grad_alpha partials
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
   __syncthreads();
-  // nominal binary mask: cD_kj independent of k, so D_j = cD_0j * popcount(pass bits of j)
+  // two-level binary mask (as cim_bwd_gx_v8_kernel, over k for each a-slice j):
+  // D_j = v1_j * popcount(pass bits in M1_j) + v2_j * popcount(pass bits in M2_j)
   bool nominal = true;
-  float cdj[NBA];
+  float dv1[NBA], dv2[NBA];
+  uint64_t dm1[NBA], dm2[NBA];
 #pragma unroll
   for (int j = 0; j < NBA; ++j) {
-    cdj[j] = cdl[j];
+    float v1 = 0.f, v2 = 0.f;
+    uint64_t m1 = 0ull, m2 = 0ull;
 #pragma unroll
-    for (int k = 1; k < NBW; ++k) nominal = nominal && (cdl[k * NBA + j] == cdj[j]);
+    for (int k = 0; k < NBW; ++k) {
+      const float c = cdl[k * NBA + j];
+      const uint64_t bit = PLS ? (1ull << (k * NBA + j)) : (1ull << (3 * (k * NBA + j)));
+      if (c == 0.f) continue;
+      if (m1 == 0ull || c == v1) { v1 = c; m1 |= bit; }
+      else if (m2 == 0ull || c == v2) { v2 = c; m2 |= bit; }
+      else nominal = false;
+    }
+    dv1[j] = sgpr_f(v1); dv2[j] = sgpr_f(v2); dm1[j] = sgpr_u64(m1); dm2[j] = sgpr_u64(m2);
   }
+  bool single = nominal && !PLS;
+#pragma unroll
+  for (int j = 0; j < NBA; ++j) single = single && dm2[j] == 0ull && dm1[j] == (uint64_t)pass_mask_j(j, NBW, NBA);
+  // pairs with a nonzero mask (grad_alpha of the others is 0 * sum = 0)
+  const uint64_t live = __builtin_amdgcn_ballot_w64(lane < NKJ && cdl[lane < NKJ ? lane : 0] != 0.f);
 
   // per tap: tile of this lane's A row (-1: channel beyond C)
   int tit[9];
@@ -585,7 +627,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
             for (int kk = 0; kk < 32; ++kk) {
               const int kj = 32 * h + kk;
-              if (kj < NKJ) {
+              if (kj < NKJ && ((live >> kj) & 1ull)) {
                 float q = 0.f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
@@ -609,15 +651,14 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         const int rowc = r16 < CPL ? r16 : 0;
 #pragma unroll 1
         for (int j = 0; j < NBA; ++j) {
-          uint64_t mj = 0ull;
-#pragma unroll
-          for (int k = 0; k < NBW; ++k) mj |= 1ull << (k * NBA + j);
+          if (dm1[j] == 0ull && dm2[j] == 0ull && nominal) continue;  // every pair of slice j masked out
           float d[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
             if (nominal) {
-              D = cdl[j] * (float)__popcll(ps[e] & mj);
+              D = dv1[j] * (float)__popcll(ps[e] & dm1[j]);
+              if (dm2[j]) D += dv2[j] * (float)__popcll(ps[e] & dm2[j]);
             } else {
               D = 0.f;
 #pragma unroll
@@ -675,8 +716,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
-            if (nominal) {
-              D = cdj[j] * (float)__popc(sv[e] & pass_mask_j(j, NBW, NBA));
+            if (single) {
+              D = dv1[j] * (float)__popc(sv[e] & pass_mask_j(j, NBW, NBA));
             } else {
               D = 0.f;
 #pragma unroll

@@ -150,8 +150,13 @@ def test_resnet20_layer_module_fullbatch(cuda_device, shape):
                            alpha_q, d["sw"].detach().numpy().reshape(1), d["sa"].detach().numpy().reshape(1),
                            float(signed))
     mc, mp = code.cpu().numpy()[sel], passed.cpu().numpy()[sel]
-    assert np.array_equal(mc, oc), f"ADC codes differ at {np.argwhere(mc != oc)[:5].tolist()}"
-    assert np.array_equal(mp, op), f"STE pass bits differ at {np.argwhere(mp != op)[:5].tolist()}"
+    # slice pairs whose binary_mask entry is 0 (the int8 wrap of the w8a8 layer, j + k >= 8) touch
+    # neither the output nor any gradient; the forward skips them and records code 0 / pass 0
+    live = (co.make_binary_mask(bits, bits, 1, 1) != 0).reshape(1, 1, bits, bits, 1, 1)
+    live = np.broadcast_to(live, mc.shape)
+    assert np.array_equal(mc[live], oc[live]), f"ADC codes differ at {np.argwhere((mc != oc) & live)[:5].tolist()}"
+    assert np.array_equal(mp[live], op[live]), f"STE pass bits differ at {np.argwhere((mp != op) & live)[:5].tolist()}"
+    assert not mc[~live].any() and not mp[~live].any()
     assert (oc != 0).mean() > 0.05 and (oc == 0).mean() > 0.05, "codes must vary for the check to bite"
 
 
