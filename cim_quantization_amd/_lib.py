@@ -18,6 +18,7 @@ ABI_VERSION = 4
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
 CIMQ_LSQ_ACCUMULATE_GRADS = 1
+CIMQ_LSQ_SKIP_TAIL = 2
 # cimq_conv_desc.adc_variant (include/cimq.h)
 CIMQ_ADC_LIBRARY = 0
 CIMQ_ADC_STOCHASTIC = 1
@@ -35,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "cimq_backward",
     "cimq_module_forward",
     "cimq_module_backward",
+    "cimq_module_backward_tail",
     "cimq_alpha_init",
     "cimq_shift_forward",
     "cimq_shift_backward",
@@ -112,6 +114,8 @@ def _bind(lib):
     lib.cimq_module_forward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 11
     lib.cimq_module_backward.restype = ctypes.c_int
     lib.cimq_module_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 16
+    lib.cimq_module_backward_tail.restype = ctypes.c_int
+    lib.cimq_module_backward_tail.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 9
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
     lib.cimq_shift_forward.restype = ctypes.c_int

@@ -67,6 +67,7 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         # parameter grads added into the existing .grad buffers inside the library (no
         # AccumulateGrad kernels); set by dist.GradBucket.own(), which owns the exchange
         self.accumulate_grads_in_place = False
+        self.tail_stream = None  # GradBucket.own(overlap=True): stream of the parameter-gradient epilogue
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
@@ -99,7 +100,8 @@ class Conv2dLSQCiM(_Conv2dQCiM):
                                   self.binary_mask, self.signed_act, self.stride, self.padding, self.dilation,
                                   self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
                                   self.xbar, self.nbits_alpha, self.accumulate_grads_in_place,
-                                  bool(self.stochastic_quant))
+                                  bool(self.stochastic_quant),
+                                  self.tail_stream if self.accumulate_grads_in_place else None)
             if self.bias is not None:
                 out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
             return out

@@ -267,6 +267,50 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   return CIMQ_OK;
 }
 
+// number of act-LSQ partials the backward leaves in ws (fused into the fast grad_x kernels, else
+// one per lsq_act_bwd_kernel block)
+static int act_parts(const Geo& g) {
+  const Plan7 p7 = v7_plan(g);
+  if (p7.ok) return g.B * p7.v.nbands;
+  const Plan3 p3 = v3_plan(g);
+  if (p3.ok) return g.B * p3.v.nbands;
+  int grid = cdiv(g.Nin, 256);
+  return grid > kLsqParts ? kLsqParts : grid;
+}
+
+// the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes
+static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
+                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
+                       float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s) {
+  const bool has_alpha = la.nbits_alpha > 0;
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  ModuleTail a;
+  a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
+  a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
+  a.scal = reinterpret_cast<const float*>(c + L.lsq_scal);
+  a.weight = weight;
+  a.alpha_cim = alpha_cim;
+  a.apart = reinterpret_cast<float*>(w + W.lsq_part);
+  a.wpart = reinterpret_cast<float*>(w + W.wpart);
+  a.gaq = reinterpret_cast<float*>(w + W.gaq);
+  a.grad_weight = grad_weight;
+  a.grad_alpha_act = grad_alpha_act;
+  a.grad_alpha_w = grad_alpha_weight;
+  a.grad_alpha_cim = grad_alpha_cim;
+  a.pp = params_of(g, const_cast<uint8_t*>(c));
+  a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
+  a.nchunks = W.nchunks_bwd;
+  a.nwb = cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64);
+  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
+  a.napart = act_parts(g);
+  a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
+  hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(a.nwb + a.nga), dim3(1024), 0, s, g, la, a);
+  CIMQ_TRY(check_hip("module_bwd_tail"));
+  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, la, a);
+  return check_hip("module_bwd_finish");
+}
+
 static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   if (!q) return fail(CIMQ_EINVAL, "null LSQ descriptor");
   if (!(q->qn_w < q->qp_w) || !(q->gscale_a > 0.f) || !(q->gscale_w > 0.f))
@@ -279,7 +323,8 @@ static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   a->gs_w = q->gscale_w;
   a->nbits_alpha = q->nbits_alpha;
   a->nalpha = g.T * g.nbw * g.nba * g.O;
-  if (q->flags & ~CIMQ_LSQ_ACCUMULATE_GRADS) return fail(CIMQ_EINVAL, "unknown LSQ flags 0x%x", q->flags);
+  if (q->flags & ~(CIMQ_LSQ_ACCUMULATE_GRADS | CIMQ_LSQ_SKIP_TAIL))
+    return fail(CIMQ_EINVAL, "unknown LSQ flags 0x%x", q->flags);
   return CIMQ_OK;
 }
 
@@ -404,31 +449,29 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
     CIMQ_TRY(check_hip("lsq_act_bwd"));
     nparts = grid;
   }
-  // one epilogue launch: grad_w + weight-LSQ backward, grad_alpha_cim, the step-size grads
-  ModuleTail a;
-  a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
-  a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
-  a.scal = scal;
-  a.weight = weight;
-  a.alpha_cim = alpha_cim;
-  a.apart = part;
-  a.wpart = reinterpret_cast<float*>(w + W.wpart);
-  a.gaq = reinterpret_cast<float*>(w + W.gaq);
-  a.grad_weight = grad_weight;
-  a.grad_alpha_act = grad_alpha_act;
-  a.grad_alpha_w = grad_alpha_weight;
-  a.grad_alpha_cim = grad_alpha_cim;
-  a.pp = params_of(g, const_cast<uint8_t*>(c));
-  a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
-  a.nchunks = W.nchunks_bwd;
-  a.nwb = cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64);
-  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
-  a.napart = nparts;
-  a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
-  hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(a.nwb + a.nga), dim3(1024), 0, s, g, la, a);
-  CIMQ_TRY(check_hip("module_bwd_tail"));
-  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, la, a);
-  return check_hip("module_bwd_finish");
+  if (nparts != act_parts(g)) return fail(CIMQ_EINVAL, "internal: act-LSQ partial count mismatch");
+  if (q->flags & CIMQ_LSQ_SKIP_TAIL) return CIMQ_OK;  // the caller runs cimq_module_backward_tail
+  return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                     grad_alpha_cim, s);
+}
+
+int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
+                              const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
+                              float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  LsqArgs la;
+  CIMQ_TRY(lsq_args(g, q, &la));
+  if (!weight || !ctx || !grad_weight || !grad_alpha_act || !grad_alpha_weight || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
+  if (has_alpha && (!alpha_cim || !grad_alpha_cim || la.nbits_alpha == 0))
+    return fail(CIMQ_EINVAL, "adc 1 / 1.5 need alpha_cim and grad_alpha_cim");
+  if (!has_alpha) la.nbits_alpha = 0;
+  return module_tail(g, la, q, reinterpret_cast<const uint8_t*>(ctx), reinterpret_cast<uint8_t*>(ws), weight,
+                     alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim,
+                     reinterpret_cast<hipStream_t>(stream));
 }
 
 int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,

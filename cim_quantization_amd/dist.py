@@ -55,22 +55,37 @@ class GradBucket:
             off += p.numel()
         self.nbytes = n * 4
         self.reattached = 0  # gradients found detached from the bucket (diagnostic)
+        self.side = None  # stream of the overlapped parameter-gradient epilogues (own(overlap=True))
         self._attach()
 
     def _attach(self):
         for p, v in zip(self.params, self.views):
             p.grad = v
 
-    def own(self, modules):
+    def own(self, modules, overlap=False):
         """Let the CiM layers among ``modules`` add their parameter gradients into this bucket
         inside libcimq (no per-parameter AccumulateGrad kernels).  Only for parameters whose
-        gradients the bucket exchanges itself: parameter hooks do not see those gradients."""
+        gradients the bucket exchanges itself: parameter hooks do not see those gradients.
+
+        ``overlap``: the layers run their parameter-gradient epilogue (slab reductions, quantiser
+        backward, step-size gradients) on the bucket's own stream, off the grad_x chain -- the
+        backward of the previous layer proceeds meanwhile.  ``join()`` (called by ``exchange()``)
+        orders the current stream after it; read the gradients only after that."""
         mine = {id(p) for p in self.params}
+        if overlap and self.side is None and self.flat.is_cuda:
+            self.side = torch.cuda.Stream(self.flat.device)
         for m in modules:
             if hasattr(m, "accumulate_grads_in_place"):
                 if all(id(p) in mine for p in m.parameters()):
                     m.accumulate_grads_in_place = True
+                    if overlap:
+                        m.tail_stream = self.side
         return self
+
+    def join(self):
+        """Order the current stream after the parameter-gradient work on the bucket's stream."""
+        if self.side is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
 
     def sync_views(self):
         """Make every ``p.grad`` the bucket view again, copying gradients that autograd put in
@@ -88,6 +103,7 @@ class GradBucket:
 
     def exchange(self, group=None):
         """Average the bucket over the ranks of ``group`` (no-op for a single process)."""
+        self.join()
         self.sync_views()
         world = _world(group)
         if world > 1:
@@ -95,6 +111,7 @@ class GradBucket:
             self.flat.mul_(1.0 / world)
 
     def zero(self):
+        self.join()
         self.flat.zero_()
         self._attach()
 

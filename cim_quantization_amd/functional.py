@@ -354,12 +354,14 @@ class _CimModuleConv(torch.autograd.Function):
     when all four ``.grad`` buffers exist as contiguous fp32 device tensors; otherwise the
     gradients are returned as usual.  Parameter hooks (e.g. DistributedDataParallel's) do not
     fire for in-place accumulated gradients, so this is for callers that own the gradient
-    exchange, like ``dist.GradBucket``."""
+    exchange, like ``dist.GradBucket``.  ``tail_stream`` (accumulate mode only): the parameter-
+    gradient epilogue runs there, off the grad_x chain, ordered after this backward by an event;
+    the bucket joins that stream before it reads the gradients (GradBucket.join)."""
 
     @staticmethod
     def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                 dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False,
-                stochastic=False):
+                stochastic=False, tail_stream=None):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
@@ -396,6 +398,7 @@ class _CimModuleConv(torch.autograd.Function):
         # them lets autograd's version counters catch an in-place change in between
         ctx.save_for_backward(x, weight, alpha_act, alpha_weight, alpha_cim)
         ctx.params = (weight, alpha_act, alpha_weight, alpha_cim) if accumulate else None
+        ctx.tail_stream = tail_stream if accumulate else None
         return out
 
     @staticmethod
@@ -424,10 +427,11 @@ class _CimModuleConv(torch.autograd.Function):
         gx = torch.empty_like(xc)
         targets = _CimModuleConv._grad_targets(ctx)
         lsq = ctx.lsq
+        side = ctx.tail_stream if targets is not None else None
         if targets is not None:
             gw, gaa, gaw, gac = targets
             lsq = _lib.make_lsq_desc(lsq.qn_w, lsq.qp_w, lsq.gscale_a, lsq.gscale_w, lsq.nbits_alpha,
-                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS)
+                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS | (_lib.CIMQ_LSQ_SKIP_TAIL if side else 0))
         else:
             gw = torch.empty_like(wc)
             gaa = torch.empty(1, device=dev, dtype=torch.float32)
@@ -441,20 +445,32 @@ class _CimModuleConv(torch.autograd.Function):
                                             gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
                                             None if gac is None else gac.data_ptr(), ws.data_ptr(), _stream()),
                    "cimq_module_backward")
+        if side is not None:
+            # parameter-gradient epilogue on the bucket's stream: the next layer's backward does not
+            # wait for it; ws / ctx stay alive until that stream is done with them
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                _lib.check(lib.cimq_module_backward_tail(ctx.desc, lsq, wc.data_ptr(),
+                                                         None if ac is None else ac.data_ptr(), cbuf.data_ptr(),
+                                                         gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
+                                                         None if gac is None else gac.data_ptr(), ws.data_ptr(),
+                                                         side.cuda_stream), "cimq_module_backward_tail")
+            for t in (ws, cbuf, wc) + ((ac,) if ac is not None else ()):
+                t.record_stream(side)
         if targets is not None:
-            return (gx,) + (None,) * 18
-        return (gx, gw, gaa, gaw, gac) + (None,) * 14
+            return (gx,) + (None,) * 19
+        return (gx, gw, gaa, gaw, gac) + (None,) * 15
 
 
 def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                     dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha,
-                    accumulate=False, stochastic=False):
+                    accumulate=False, stochastic=False, tail_stream=None):
     """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
     the three step-size parameters (alpha_act and alpha_weight are 1-element tensors).
-    ``accumulate``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC."""
+    ``accumulate`` / ``tail_stream``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC."""
     return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
                                 padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
-                                nbits_alpha, accumulate, stochastic)
+                                nbits_alpha, accumulate, stochastic, tail_stream)
 
 
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,

@@ -70,6 +70,10 @@ extern "C" {
 #define CIMQ_LSQ_ACCUMULATE_GRADS 1 /* cimq_module_backward adds the parameter gradients into
                                        grad_weight / grad_alpha_* (torch's AccumulateGrad,
                                        grad = grad + new) instead of overwriting them */
+#define CIMQ_LSQ_SKIP_TAIL 2        /* cimq_module_backward stops after grad_x and the per-chunk
+                                       grad_w / grad_alpha partials (left in ws); the caller runs
+                                       cimq_module_backward_tail later, e.g. on a second stream
+                                       (the parameter gradients are off the grad_x chain) */
 
 typedef struct cimq_conv_desc {
   int32_t batch, in_channels, in_h, in_w; /* B, C, H, W */
@@ -156,6 +160,15 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
                          const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,
                          const void* ctx, float* grad_x, float* grad_weight, float* grad_alpha_act,
                          float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
+
+/* The parameter-gradient epilogue of cimq_module_backward (slab reductions of grad_w and
+ * grad_alpha, the weight / alpha_cim quantiser backward, the two step-size gradients) for a
+ * backward run with CIMQ_LSQ_SKIP_TAIL: ``ctx`` and ``ws`` are that call's, unchanged, and the
+ * stream must be ordered after it.  Replaces the torch autograd of lsq.py:547-571 into the
+ * parameters.  q->flags as that call's (CIMQ_LSQ_ACCUMULATE_GRADS honoured). */
+int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
+                              const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
+                              float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
 
 /* First-step alpha_cim initialisation (lsq.py:557-563 with get_analog_partial_sums_signed,
  * lsq.py:35-87): alpha_init[1,T,nbw,nba,1,O] = 2*mean_{b,p}|ps*sw*sa| / sqrt(Qp_adc), zeros

@@ -43,7 +43,7 @@ if os.environ.get("CIMQ_EXP_VARIANTS"):
 
 
 def lib_path(name):
-    return os.path.join(REPO, "exp", f"libcimq_{name}.so")
+    return os.path.join(REPO, os.environ.get("CIMQ_EXP_DIR", "exp"), f"libcimq_{name}.so")
 
 
 def do_build():
