@@ -462,10 +462,19 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   // pairs with a nonzero mask (grad_alpha of the others is 0 * sum = 0)
   const uint64_t live = __builtin_amdgcn_ballot_w64(lane < NKJ && cdl[lane < NKJ ? lane : 0] != 0.f);
 
-  // per tap: tile of this lane's A row (-1: channel beyond C)
-  int tit[9];
+  // A rows: 16 consecutive weight rows f per MFMA row group -- f = cb*16*KHW + 16*gr + (lane & 15),
+  // f = (c, kh, kw) -- so a crossbar tile's rows of this channel block take ceil(rows / 16) groups
+  // (tile boundaries are multiples of 16 here: xbar and 16*KHW are).  Per lane and group: the
+  // plane offset of its row's (kw, channel) times 4 plus kh, or -1 past C; per group: its tile.
+  int gpk[9], gtile[9];
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp) tit[tp] = (tp < KHW && ca < g.C) ? (ca * KHW + tp) / g.xbar : -1;
+  for (int gr = 0; gr < 9; ++gr) {
+    const int f0 = cb * 16 * KHW + 16 * gr, f = f0 + r16;
+    const int c = f / KHW, tap = f - c * KHW, kh = tap / 3, kw = tap - 3 * kh;
+    gpk[gr] = (c < g.C) ? (((kw * CPL + (c - cb * 16)) * v.CPITCH) << 2) | kh : -1;
+    gtile[gr] = (f0 < g.C * KHW) ? f0 / g.xbar : -1;
+  }
+  (void)ca;
 
   v4f acc[9];
 #pragma unroll
@@ -648,7 +657,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           const uint2 a = s2[e * es];
           ps[e] = (uint64_t)a.x | ((uint64_t)a.y << 32);
         }
-        const int rowc = r16 < CPL ? r16 : 0;
 #pragma unroll 1
         for (int j = 0; j < NBA; ++j) {
           if (dm1[j] == 0ull && dm2[j] == 0ull && nominal) continue;  // every pair of slice j masked out
@@ -669,17 +677,18 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           v8bf bh, bm, bq;
           split3x8(d, bh, bm, bq);
 #pragma unroll
-          for (int tp = 0; tp < 9; ++tp) {
-            const int kh = tp / 3, kw = tp - 3 * (tp / 3);
-            const int sl = slot_kh[kh];
-            const bool ok = (tit[tp] == i) && sl >= 0;
-            const __bf16* src = pl + ((size_t)(j * 3 + kw) * CPL + rowc) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
+          for (int gr = 0; gr < 9; ++gr) {
+            if (gtile[gr] != i) continue;  // uniform: the row groups of tile i
+            const int kh = gpk[gr] & 3;
+            const int sl = kh == 0 ? slot_kh[0] : (kh == 1 ? slot_kh[1] : slot_kh[2]);
+            const bool ok = gpk[gr] >= 0 && sl >= 0;
+            const __bf16* src = pl + (size_t)j * 3 * CPL * v.CPITCH + (ok ? (gpk[gr] >> 2) + sl * Wo : 0) + ow0;
             v4i a4 = *reinterpret_cast<const v4i*>(src);
             a4 = ok ? a4 : v4i{0, 0, 0, 0};
             const v8bf a = as_v8bf(a4);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[tp], 0, 0, 0);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[tp], 0, 0, 0);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[tp], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[gr], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[gr], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[gr], 0, 0, 0);
           }
         }
       } else if (!PLS && tl < ntl) {
@@ -727,13 +736,13 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           }
           split3x8(d, bh[j], bm[j], bq[j]);
         }
-        // A fragments of a tap (rows of other tiles and kernel rows outside the image are
-        // zeroed by a select, no branch)
-        auto read_tap = [&](int tp, v4i (&dst)[NBA]) {
-          const int kh = tp / 3, kw = tp - 3 * (tp / 3);
-          const int sl = slot_kh[kh];
-          const bool ok = (tit[tp] == i) && sl >= 0;
-          const __bf16* src = pl + ((size_t)kw * CPL + (r16 < CPL ? r16 : 0)) * v.CPITCH + (sl < 0 ? 0 : sl) * Wo + ow0;
+        // A fragments of a row group (rows past C and kernel rows outside the image are zeroed by
+        // a select, no branch)
+        auto read_group = [&](int gr, v4i (&dst)[NBA]) {
+          const int kh = gpk[gr] & 3;
+          const int sl = kh == 0 ? slot_kh[0] : (kh == 1 ? slot_kh[1] : slot_kh[2]);
+          const bool ok = gpk[gr] >= 0 && sl >= 0;
+          const __bf16* src = pl + (ok ? (gpk[gr] >> 2) + sl * Wo : 0) + ow0;
 #pragma unroll
           for (int j = 0; j < NBA; ++j) {
             const v4i a = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * CPL * v.CPITCH);
@@ -741,19 +750,20 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           }
         };
 #pragma unroll
-        for (int tp = 0; tp < 9; ++tp) {
+        for (int gr = 0; gr < 9; ++gr) {
+          if (gtile[gr] != i) continue;  // uniform: the row groups of tile i
           v4i acur[NBA];
-          read_tap(tp, acur);
+          read_group(gr, acur);
 #ifndef CIMQ_EXP_GW_NOMFMA
 #pragma unroll
           for (int j = 0; j < NBA; ++j) {
             const v8bf a = as_v8bf(acur[j]);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[tp], 0, 0, 0);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[tp], 0, 0, 0);
-            acc[tp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[tp], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[gr], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[gr], 0, 0, 0);
+            acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[gr], 0, 0, 0);
           }
 #else
-          acc[tp][0] += (float)acur[0][0];
+          acc[gr][0] += (float)acur[0][0];
 #endif
         }
       }
@@ -762,18 +772,18 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   // reduce the four waves' partials through LDS (the planes are free now; plain stores, one
   // region per wave -- LDS float atomics are slow), then write the slabs
   __syncthreads();
-  float* gred = reinterpret_cast<float*>(pl);  // [4 waves][9 taps][16 c][16 o]
+  float* gred = reinterpret_cast<float*>(pl);  // [4 waves][9 row groups][16 rows f][16 o]
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp)
+  for (int gr = 0; gr < 9; ++gr)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gred[((wave * 9 + tp) * 16 + 4 * g4 + r) * 16 + r16] = acc[tp][r];
+    for (int r = 0; r < 4; ++r) gred[((wave * 9 + gr) * 16 + 4 * g4 + r) * 16 + r16] = acc[gr][r];
   __syncthreads();
   const int FR = g.FBT * 16;
   for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) {
-    const int tp = t >> 8, cr = (t >> 4) & 15, oc = t & 15;
-    const int c = cb * 16 + cr;
-    if (c < g.C) {
-      const int f = c * KHW + tp, i = f / g.xbar, fl = f - i * g.xbar;
+    const int oc = t & 15;
+    const int f = cb * 16 * KHW + (t >> 4);  // row group t >> 8, row (t >> 4) & 15
+    if (f < g.C * KHW) {
+      const int i = f / g.xbar, fl = f - i * g.xbar;
       const float sum = (gred[t] + gred[9 * 256 + t]) + (gred[2 * 9 * 256 + t] + gred[3 * 9 * 256 + t]);
       gw_slab[(((size_t)chunk * g.T + i) * FR + fl) * g.Opad + ob * 16 + oc] = sum;
     }
