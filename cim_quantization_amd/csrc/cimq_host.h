@@ -327,7 +327,8 @@ inline Plan7 v7_plan(const Geo& g) {
   // instantiated slice pairs: w3a3 / w2a2 (interleaved state words) and w8a8 (plane state words)
   if (g.NBP == 4 && !((g.nbw == 3 && g.nba == 3) || (g.nbw == 2 && g.nba == 2))) return p;
   // w8a8: one 16-channel output block (the first conv of the CIFAR ResNets; wider blocks spill)
-  if (g.NBP == 8 && !(g.nbw == 8 && g.nba == 8 && g.OB16 == 1)) return p;
+  // plane words: the w8a8 first layer only (grad_w: at most two 16-row groups, C*KHW <= 32)
+  if (g.NBP == 8 && !(g.nbw == 8 && g.nba == 8 && g.OB16 == 1 && g.C * g.KHW <= 32)) return p;
   if (g.O % 16 != 0 || !(g.OB16 == 1 || g.OB16 == 2 || g.OB16 == 4)) return p;
   // 3x3, stride 1, pad 1 ("same" conv: every CiM conv of the CIFAR ResNets but the downsampling ones)
   if (g.KH != 3 || g.KW != 3 || g.SH != g.SW || g.SH > 2 || g.PH != 1 || g.PW != 1) return p;

@@ -130,33 +130,19 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
   const int Wo = 1 << v.lw;
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cel[t] = pp.ckj[NKJ + t];
   __syncthreads();
-  // two-level binary mask: per slice k, every cE_kj is 0, v1_k or v2_k, so that
-  // E_k = v1_k * popcount(pass bits in M1_k) + v2_k * popcount(pass bits in M2_k).  The plain
-  // mask has one level (cE_kj = 2^(bsw*k) for every j); the int8-wrapped 8-bit mask two
-  // (2^k, and -2^k at j + k = 7) plus zeros (j + k >= 8).  Bits are in state-word coordinates.
-  bool nominal = true;
-  float ev1[NBW], ev2[NBW];
-  uint64_t em1[NBW], em2[NBW];
-#pragma unroll
-  for (int k = 0; k < NBW; ++k) {
-    float v1 = 0.f, v2 = 0.f;
-    uint64_t m1 = 0ull, m2 = 0ull;
-#pragma unroll
-    for (int j = 0; j < NBA; ++j) {
-      const float c = cel[k * NBA + j];
-      const uint64_t bit = PLS ? (1ull << (k * NBA + j)) : (1ull << (3 * (k * NBA + j)));
-      if (c == 0.f) continue;
-      if (m1 == 0ull || c == v1) { v1 = c; m1 |= bit; }
-      else if (m2 == 0ull || c == v2) { v2 = c; m2 |= bit; }
-      else nominal = false;
-    }
-    ev1[k] = sgpr_f(v1); ev2[k] = sgpr_f(v2); em1[k] = sgpr_u64(m1); em2[k] = sgpr_u64(m2);
+  // standard binary masks (_quan_base.py:207-214), checked once per block: the plain mask
+  // (cE_kj = 2^(bsw*k) for every j) gives E_k = 2^(bsw*k) * popcount(pass bits of slice k);
+  // the int8-wrapped 8-bit mask (plane words) cE_kj = 2^k for j + k < 7, -2^k at j + k = 7 and
+  // 0 beyond gives E_k = 2^k * (popcount(pass bits j < 7 - k) - pass bit j = 7 - k).  Both are
+  // exact (small integers times a power of two); any other mask takes the per-pair sum.
+  bool std_mask;
+  {
+    const int kl = lane < NKJ ? lane / NBA : 0, jl = lane < NKJ ? lane - kl * NBA : 0;
+    const float ce = PLS ? ((kl + jl < 7) ? ldexpf(1.f, kl) : (kl + jl == 7 ? -ldexpf(1.f, kl) : 0.f))
+                         : ldexpf(1.f, g.bsw * kl);
+    std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cel[lane < NKJ ? lane : 0] != ce) == 0ull;
+    if (PLS && (NBW != 8 || NBA != 8)) std_mask = false;
   }
-  // interleaved words (<= 10 pairs): the plain one-level mask takes the compile-time pass masks,
-  // anything else the per-pair sum; plane words (w8a8) use the two-level form
-  bool single = nominal && !PLS;
-#pragma unroll
-  for (int k = 0; k < NBW; ++k) single = single && em2[k] == 0ull && em1[k] == (uint64_t)pass_mask_k(k, NBA);
   const float scale = sw / (float)NBA;
   float gpart = 0.f;
   int done = r0 - 1;
@@ -214,16 +200,16 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
             float E;
             if constexpr (PLS) {
               const uint32_t fld = (uint32_t)(sp[ob][r] >> (k * NBA)) & ((1u << NBA) - 1u);
-              if (nominal) {
-                E = ev1[k] * (float)__popcll(sp[ob][r] & em1[k]);
-                if (em2[k]) E += ev2[k] * (float)__popcll(sp[ob][r] & em2[k]);
+              if (std_mask) {
+                const int n = __popc(fld & ((1u << (7 - k)) - 1u)) - (int)((fld >> (7 - k)) & 1u);
+                E = (float)(n * (1 << k));
               } else {
                 E = 0.f;
-#pragma unroll
+#pragma unroll 1
                 for (int j = 0; j < NBA; ++j) E += ((fld >> j) & 1u) ? cel[k * NBA + j] : 0.f;
               }
-            } else if (single) {
-              E = ev1[k] * (float)__popc(sv[ob][r] & pass_mask_k(k, NBA));
+            } else if (std_mask) {
+              E = ldexpf((float)__popc(sv[ob][r] & pass_mask_k(k, NBA)), g.bsw * k);
             } else {
               E = 0.f;
 #pragma unroll
@@ -412,6 +398,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
                                                             float* __restrict__ ga_slab) {
   constexpr int NKJ = NBW * NBA;
   constexpr bool PLS = NKJ > 10;  // plane state words (cim_fwd_v3_kernel PLF)
+  constexpr int NGR = PLS ? 2 : 9;  // row groups of 16 per channel block (w8a8 plan: C*KHW <= 32)
   typedef typename std::conditional<(NBA > 4), uint2, uint32_t>::type XW;  // ctx slice bytes (NBP)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int chunk = blockIdx.x, pair = blockIdx.y;
@@ -436,29 +423,18 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   float* red = reinterpret_cast<float*>(cur);  // [4 waves][NTL][NKJ][16] grad_alpha partials
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
   __syncthreads();
-  // two-level binary mask (as cim_bwd_gx_v8_kernel, over k for each a-slice j):
-  // D_j = v1_j * popcount(pass bits in M1_j) + v2_j * popcount(pass bits in M2_j)
-  bool nominal = true;
-  float dv1[NBA], dv2[NBA];
-  uint64_t dm1[NBA], dm2[NBA];
-#pragma unroll
-  for (int j = 0; j < NBA; ++j) {
-    float v1 = 0.f, v2 = 0.f;
-    uint64_t m1 = 0ull, m2 = 0ull;
-#pragma unroll
-    for (int k = 0; k < NBW; ++k) {
-      const float c = cdl[k * NBA + j];
-      const uint64_t bit = PLS ? (1ull << (k * NBA + j)) : (1ull << (3 * (k * NBA + j)));
-      if (c == 0.f) continue;
-      if (m1 == 0ull || c == v1) { v1 = c; m1 |= bit; }
-      else if (m2 == 0ull || c == v2) { v2 = c; m2 |= bit; }
-      else nominal = false;
-    }
-    dv1[j] = sgpr_f(v1); dv2[j] = sgpr_f(v2); dm1[j] = sgpr_u64(m1); dm2[j] = sgpr_u64(m2);
+  // standard binary masks, as cim_bwd_gx_v8_kernel, now summed over k for each a-slice j: the
+  // plain mask (cD_kj = 2^(bsa*j)) gives D_j = 2^(bsa*j) * popcount(pass bits of slice j); the
+  // int8-wrapped 8-bit mask (cD_kj = 2^j for k < 7 - j, -2^j at k = 7 - j, 0 beyond) gives
+  // D_j = 2^j * (popcount(pass bits k < 7 - j) - pass bit k = 7 - j).  Else the per-pair sum.
+  bool std_mask;
+  {
+    const int kl = lane < NKJ ? lane / NBA : 0, jl = lane < NKJ ? lane - kl * NBA : 0;
+    const float ce = PLS ? ((kl + jl < 7) ? ldexpf(1.f, jl) : (kl + jl == 7 ? -ldexpf(1.f, jl) : 0.f))
+                         : ldexpf(1.f, g.bsa * jl);
+    std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cdl[lane < NKJ ? lane : 0] != ce) == 0ull;
+    if (PLS && (NBW != 8 || NBA != 8)) std_mask = false;
   }
-  bool single = nominal && !PLS;
-#pragma unroll
-  for (int j = 0; j < NBA; ++j) single = single && dm2[j] == 0ull && dm1[j] == (uint64_t)pass_mask_j(j, NBW, NBA);
   // pairs with a nonzero mask (grad_alpha of the others is 0 * sum = 0)
   const uint64_t live = __builtin_amdgcn_ballot_w64(lane < NKJ && cdl[lane < NKJ ? lane : 0] != 0.f);
 
@@ -466,9 +442,9 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   // f = (c, kh, kw) -- so a crossbar tile's rows of this channel block take ceil(rows / 16) groups
   // (tile boundaries are multiples of 16 here: xbar and 16*KHW are).  Per lane and group: the
   // plane offset of its row's (kw, channel) times 4 plus kh, or -1 past C; per group: its tile.
-  int gpk[9], gtile[9];
+  int gpk[NGR], gtile[NGR];
 #pragma unroll
-  for (int gr = 0; gr < 9; ++gr) {
+  for (int gr = 0; gr < NGR; ++gr) {
     const int f0 = cb * 16 * KHW + 16 * gr, f = f0 + r16;
     const int c = f / KHW, tap = f - c * KHW, kh = tap / 3, kw = tap - 3 * kh;
     gpk[gr] = (c < g.C) ? (((kw * CPL + (c - cb * 16)) * v.CPITCH) << 2) | kh : -1;
@@ -476,9 +452,9 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   }
   (void)ca;
 
-  v4f acc[9];
+  v4f acc[NGR];
 #pragma unroll
-  for (int tp = 0; tp < 9; ++tp) acc[tp] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int tp = 0; tp < NGR; ++tp) acc[tp] = v4f{0.f, 0.f, 0.f, 0.f};
   // grad_alpha partials accumulate in LDS, one region per wave: red[wave][tl][kj][16 o]
   for (int t = threadIdx.x; t < 4 * NTL * NKJ * 16; t += blockDim.x) red[t] = 0.f;
 
@@ -623,7 +599,11 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         const int i = i_lo + tl;
         const uint2* s2 = reinterpret_cast<const uint2*>(st) + ((size_t)i * g.M + mk8) * g.O * 3 + (size_t)o * 3;
         const size_t es = (size_t)g.O * 3;
+#ifdef CIMQ_EXP_GW_NOGA
+        if (false) {
+#else
         if (((i * g.xbar) / KHW) / 16 == cb) {
+#endif
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             uint32_t nzw[8], ngw[8];
@@ -633,21 +613,22 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
               nzw[e] = h ? a.y : a.x;
               ngw[e] = h ? c2.y : c2.x;
             }
-#pragma unroll
-            for (int kk = 0; kk < 32; ++kk) {
+            // the live pairs of this half, lowest first (a uniform loop: runtime bit offsets)
+            uint32_t lv = (uint32_t)(live >> (32 * h));
+            while (lv != 0u) {
+              const int kk = __builtin_ctz(lv);
+              lv &= lv - 1u;
               const int kj = 32 * h + kk;
-              if (kj < NKJ && ((live >> kj) & 1ull)) {
-                float q = 0.f;
+              float q = 0.f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                  const uint32_t nzm = (uint32_t)(((int)(nzw[e] << (31 - kk))) >> 31);
-                  const uint32_t sgn = (ngw[e] << (31 - kk)) & 0x80000000u;
-                  q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
-                }
-                q += __shfl_xor(q, 16);
-                q += __shfl_xor(q, 32);
-                if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
+              for (int e = 0; e < 8; ++e) {
+                const uint32_t nzm = (uint32_t)(((int)(nzw[e] << (31 - kk))) >> 31);
+                const uint32_t sgn = (ngw[e] << (31 - kk)) & 0x80000000u;
+                q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
               }
+              q += __shfl_xor(q, 16);
+              q += __shfl_xor(q, 32);
+              if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
             }
           }
         }
@@ -659,17 +640,29 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         }
 #pragma unroll 1
         for (int j = 0; j < NBA; ++j) {
-          if (dm1[j] == 0ull && dm2[j] == 0ull && nominal) continue;  // every pair of slice j masked out
+          // pass bits k*8 + j of the k < 7 - j pairs, and of the k = 7 - j pair (uniform)
+          const uint64_t m1 = (0x0101010101010101ull & ((1ull << (8 * (7 - j))) - 1ull)) << j;
+          const int nb = 56 - 7 * j;
+          if (!std_mask) {
+            bool any = false;
+            for (int k = 0; k < NBW; ++k) any = any || cdl[k * NBA + j] != 0.f;
+            if (!any) continue;  // every pair of slice j masked out
+          }
           float d[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
-            if (nominal) {
-              D = dv1[j] * (float)__popcll(ps[e] & dm1[j]);
-              if (dm2[j]) D += dv2[j] * (float)__popcll(ps[e] & dm2[j]);
+#ifdef CIMQ_EXP_GW_NOD
+            if (true) {
+              D = (float)(uint32_t)ps[e];
+            } else
+#endif
+            if (std_mask) {
+              const int n = __popcll(ps[e] & m1) - (int)((ps[e] >> nb) & 1ull);
+              D = (float)(n * (1 << j));
             } else {
               D = 0.f;
-#pragma unroll
+#pragma unroll 1
               for (int k = 0; k < NBW; ++k) D += ((ps[e] >> (k * NBA + j)) & 1ull) ? cdl[k * NBA + j] : 0.f;
             }
             d[e] = gv[e] * D;
@@ -677,7 +670,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           v8bf bh, bm, bq;
           split3x8(d, bh, bm, bq);
 #pragma unroll
-          for (int gr = 0; gr < 9; ++gr) {
+          for (int gr = 0; gr < NGR; ++gr) {
             if (gtile[gr] != i) continue;  // uniform: the row groups of tile i
             const int kh = gpk[gr] & 3;
             const int sl = kh == 0 ? slot_kh[0] : (kh == 1 ? slot_kh[1] : slot_kh[2]);
@@ -686,9 +679,13 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             v4i a4 = *reinterpret_cast<const v4i*>(src);
             a4 = ok ? a4 : v4i{0, 0, 0, 0};
             const v8bf a = as_v8bf(a4);
+#ifndef CIMQ_EXP_GW_NOMFMA
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[gr], 0, 0, 0);
+#else
+            acc[gr][0] += (float)a4[0] + (float)bh[0] + (float)bm[1] + (float)bq[2];
+#endif
           }
         }
       } else if (!PLS && tl < ntl) {
@@ -725,8 +722,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
-            if (single) {
-              D = dv1[j] * (float)__popc(sv[e] & pass_mask_j(j, NBW, NBA));
+            if (std_mask) {
+              D = ldexpf((float)__popc(sv[e] & pass_mask_j(j, NBW, NBA)), g.bsa * j);
             } else {
               D = 0.f;
 #pragma unroll
@@ -750,7 +747,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           }
         };
 #pragma unroll
-        for (int gr = 0; gr < 9; ++gr) {
+        for (int gr = 0; gr < NGR; ++gr) {
           if (gtile[gr] != i) continue;  // uniform: the row groups of tile i
           v4i acur[NBA];
           read_group(gr, acur);
@@ -772,19 +769,19 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   // reduce the four waves' partials through LDS (the planes are free now; plain stores, one
   // region per wave -- LDS float atomics are slow), then write the slabs
   __syncthreads();
-  float* gred = reinterpret_cast<float*>(pl);  // [4 waves][9 row groups][16 rows f][16 o]
+  float* gred = reinterpret_cast<float*>(pl);  // [4 waves][NGR row groups][16 rows f][16 o]
 #pragma unroll
-  for (int gr = 0; gr < 9; ++gr)
+  for (int gr = 0; gr < NGR; ++gr)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gred[((wave * 9 + gr) * 16 + 4 * g4 + r) * 16 + r16] = acc[gr][r];
+    for (int r = 0; r < 4; ++r) gred[((wave * NGR + gr) * 16 + 4 * g4 + r) * 16 + r16] = acc[gr][r];
   __syncthreads();
   const int FR = g.FBT * 16;
-  for (int t = threadIdx.x; t < 9 * 256; t += blockDim.x) {
+  for (int t = threadIdx.x; t < NGR * 256; t += blockDim.x) {
     const int oc = t & 15;
     const int f = cb * 16 * KHW + (t >> 4);  // row group t >> 8, row (t >> 4) & 15
     if (f < g.C * KHW) {
       const int i = f / g.xbar, fl = f - i * g.xbar;
-      const float sum = (gred[t] + gred[9 * 256 + t]) + (gred[2 * 9 * 256 + t] + gred[3 * 9 * 256 + t]);
+      const float sum = (gred[t] + gred[NGR * 256 + t]) + (gred[2 * NGR * 256 + t] + gred[3 * NGR * 256 + t]);
       gw_slab[(((size_t)chunk * g.T + i) * FR + fl) * g.Opad + ob * 16 + oc] = sum;
     }
   }

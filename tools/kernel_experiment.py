@@ -23,6 +23,9 @@ VARIANTS = {
     "gw_noga": ["CIMQ_EXP_GW_NOGA"],
     "gw_nomfma": ["CIMQ_EXP_GW_NOMFMA"],
     "gw_nostage": ["CIMQ_EXP_GW_NOSTAGE"],
+    "gw_nod": ["CIMQ_EXP_GW_NOD"],
+    "gw_noga_nomfma": ["CIMQ_EXP_GW_NOGA", "CIMQ_EXP_GW_NOMFMA"],
+    "gw_noga_nomfma_nod": ["CIMQ_EXP_GW_NOGA", "CIMQ_EXP_GW_NOMFMA", "CIMQ_EXP_GW_NOD"],
     "gx_nomfma": ["CIMQ_EXP_GX_NOMFMA"],
     "gx_noring": ["CIMQ_EXP_GX_NORING"],
     "fwd_nost": ["CIMQ_EXP_FWD_NOST"],
@@ -48,7 +51,7 @@ def lib_path(name):
 
 def do_build():
     from cim_quantization_amd import build as B
-    os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
+    os.makedirs(os.path.dirname(lib_path("base")), exist_ok=True)
     with cf.ThreadPoolExecutor(len(VARIANTS)) as ex:
         futs = {ex.submit(B.build, True, False, lib_path(n), list(d) + ["CIMQ_TUNING"]): n
                 for n, d in VARIANTS.items()}
