@@ -49,6 +49,10 @@ def build(force: bool = False, verbose: bool = True, out: str = OUT, defines=())
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-pass-failed"]
+    # MFMA results straight into arch VGPRs: the epilogues read every partial sum / product,
+    # and the default AGPR form costs one v_accvgpr_read per element (about 9 % of the forward's
+    # VALU issue per slice pair)
+    flags += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
     flags += [f"-D{d}" for d in defines]
     objdir = out + ".objs"
     os.makedirs(objdir, exist_ok=True)

@@ -326,6 +326,105 @@ __device__ inline void lsq_finish_block(const LsqArgs& q, const ModuleTail& a, f
   }
 }
 
+// The epilogue's last step (module_bwd_finish_kernel): alpha_cim's quantiser backward and the
+// two step-size gradients from the partials module_bwd_tail_kernel left.  It is a chain of
+// dependent memory round trips, so with nalpha <= 8 * 1024 every load is issued up front
+// (alpha_cim, d loss / d alpha_q, the accumulated gradient, both partial sets), the two
+// reductions share one pass, and the second sweep runs from registers.  Same per-thread
+// order, same sums as the two-sweep form (alpha_cim_bwd_block + lsq_finish_block).
+template <int N>
+__device__ inline void block_sumn(float (&v)[N], float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], o);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < N; ++i) red[w * N + i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = red[i];
+  for (int k = 1; k < nw; ++k)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += red[k * N + i];
+  __syncthreads();
+}
+
+__device__ inline void module_finish_block(const LsqArgs& q, const ModuleTail& a, float* red) {
+  constexpr int PER = 8;
+  if (q.nbits_alpha > 0 && q.nalpha > PER * (int)blockDim.x) {  // large alpha_cim: two sweeps
+    alpha_cim_bwd_block(q, a, red);
+    lsq_finish_block(q, a, red);
+    return;
+  }
+  const bool has_a = q.nbits_alpha > 0;
+  float av[PER], gv[PER], old[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + u * (int)blockDim.x;
+    const bool in = has_a && e < q.nalpha;
+    av[u] = in ? a.alpha_cim[e] : 0.f;
+    gv[u] = in ? a.gaq[e] : 0.f;
+    old[u] = (in && a.accum) ? a.grad_alpha_cim[e] : 0.f;
+  }
+  float m = 0.f, d = 0.f, sp = 0.f;
+  for (int t = threadIdx.x; t < a.nwb; t += blockDim.x) {
+    m += a.wpart[2 * t];
+    d += a.wpart[2 * t + 1];
+  }
+  for (int t = threadIdx.x; t < a.napart; t += blockDim.x) sp += a.apart[t];
+  const float scale = has_a ? a.scal[2] : 1.f, mx = has_a ? a.scal[3] : 0.f, mn = has_a ? a.scal[4] : 0.f;
+  const float qp_al = (float)((1 << q.nbits_alpha) - 1);
+  const float N = (float)((1 << q.nbits_alpha) - 2);
+  float s_mul = 0.f, s_div = 0.f, cmax = 0.f, cmin = 0.f;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + u * (int)blockDim.x;
+    if (has_a && e < q.nalpha) {  // as alpha_cim_bwd_block's first sweep
+      const float v = av[u];
+      const float t = v / scale;
+      const float rp = round_pass_value(t);
+      const float c = clamp_nan(rp, 1.f, qp_al);
+      const bool pass = (rp >= 1.f) && (rp <= qp_al);
+      const float gt = pass ? gv[u] * scale : 0.f;
+      s_mul += gv[u] * c;
+      s_div += -gt * (t / scale);
+      cmax += ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f;
+      cmin += ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f;
+    }
+  }
+  float r[8] = {s_mul, s_div, cmax, cmin, m, d, sp, 0.f};
+  block_sumn<8>(r, red);
+  if (has_a) {
+    const float gdiff = (r[0] + r[1]) / N;  // d loss / d scale, then DivBackward of (max - min) / N
+    const float pmax = gdiff / r[2], pmin = -gdiff / r[3];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = threadIdx.x + u * (int)blockDim.x;
+      if (e < q.nalpha) {
+        const float v = av[u];
+        const float t = v / scale;
+        const float rp = round_pass_value(t);
+        const bool pass = (rp >= 1.f) && (rp <= qp_al);
+        const float gt = pass ? gv[u] * scale : 0.f;
+        const bool ismin = (mn != mn) ? (v != v) : (v == mn);
+        const bool ismax = (mx != mx) ? (v != v) : (v == mx);
+        float rr = gt / scale;
+        rr = rr + (ismin ? pmin : 0.f);
+        rr = rr + (ismax ? pmax : 0.f);
+        a.grad_alpha_cim[e] = a.accum ? old[u] + rr : rr;
+      }
+    }
+  }
+  if (threadIdx.x == 0) {  // as lsq_finish_block
+    const float gw = (r[4] + r[5]) * q.gs_w;
+    const float ga = r[6] * q.gs_a;
+    a.grad_alpha_w[0] = a.accum ? a.grad_alpha_w[0] + gw : gw;
+    a.grad_alpha_act[0] = a.accum ? a.grad_alpha_act[0] + ga : ga;
+  }
+}
+
 __global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q, ModuleTail a) {
   __shared__ float red[1024];
   const int b = (int)blockIdx.x;
@@ -333,14 +432,13 @@ __global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q,
   else galpha_role(g, a, b - a.nwb, red);
 }
 
-// One block: alpha_cim's quantiser backward and the two step-size gradients, from the
-// partials module_bwd_tail_kernel left (a kernel boundary orders them across the XCDs'
-// L2s, which a last-block-done ticket would have to buy with an L2 writeback per block).
+// One block: the epilogue's last step after the kernel boundary (which orders the partials
+// across the XCDs' L2s).  Fusing it into module_bwd_tail_kernel behind a last-block ticket
+// measured slower: 18.3 us per layer for the fused launch against 5.8 + 7.5 us for the two
+// (the per-block agent-scope release costs more than the boundary it replaces).
 __global__ __launch_bounds__(1024) void module_bwd_finish_kernel(LsqArgs q, ModuleTail a) {
-  __shared__ float4 red4[16];
-  float* red = reinterpret_cast<float*>(red4);
-  if (q.nbits_alpha > 0) alpha_cim_bwd_block(q, a, red);
-  lsq_finish_block(q, a, red);
+  __shared__ __attribute__((aligned(16))) float red[16 * 8];
+  module_finish_block(q, a, red);
 }
 
 // layout changes for the general (non-fast-path) kernels in module mode
