@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -42,6 +42,12 @@ EXPORTED_SYMBOLS = (
     "cimq_shift_backward",
     "cimq_debug_partial_sums",
     "cimq_debug_state_codes",
+    "cimq_lsq_quantize_forward",
+    "cimq_lsq_quantize_workspace_bytes",
+    "cimq_lsq_quantize_backward",
+    "cimq_qconv_sizes",
+    "cimq_qconv_forward",
+    "cimq_qconv_backward_scales",
     "cimq_profile_start",
     "cimq_profile_stop",
 )
@@ -81,6 +87,21 @@ class LsqDesc(ctypes.Structure):
     _fields_ = [("qn_w", ctypes.c_float), ("qp_w", ctypes.c_float), ("gscale_a", ctypes.c_float),
                 ("gscale_w", ctypes.c_float), ("nbits_alpha", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("reserved", ctypes.c_int32 * 2)]
+
+
+class QConvDesc(ctypes.Structure):
+    """Mirror of ``cimq_qconv_desc``."""
+
+    _fields_ = [
+        ("batch", ctypes.c_int32), ("in_channels", ctypes.c_int32),
+        ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32),
+        ("out_channels", ctypes.c_int32), ("kernel_h", ctypes.c_int32), ("kernel_w", ctypes.c_int32),
+        ("stride_h", ctypes.c_int32), ("stride_w", ctypes.c_int32),
+        ("pad_h", ctypes.c_int32), ("pad_w", ctypes.c_int32),
+        ("dilation_h", ctypes.c_int32), ("dilation_w", ctypes.c_int32), ("groups", ctypes.c_int32),
+        ("code_min", ctypes.c_int32), ("code_max", ctypes.c_int32),
+        ("has_bias", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
 
 
 class Sizes(ctypes.Structure):
@@ -126,6 +147,20 @@ def _bind(lib):
     lib.cimq_debug_partial_sums.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
     lib.cimq_debug_state_codes.restype = ctypes.c_int
     lib.cimq_debug_state_codes.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 4
+    _F, _LL, _I = ctypes.c_float, ctypes.c_longlong, ctypes.c_int
+    lib.cimq_lsq_quantize_forward.restype = ctypes.c_int
+    lib.cimq_lsq_quantize_forward.argtypes = [_VP, _LL, _VP, _F, _F, _I, _VP, _VP]
+    lib.cimq_lsq_quantize_workspace_bytes.restype = ctypes.c_size_t
+    lib.cimq_lsq_quantize_workspace_bytes.argtypes = [_LL]
+    lib.cimq_lsq_quantize_backward.restype = ctypes.c_int
+    lib.cimq_lsq_quantize_backward.argtypes = [_VP, _LL, _VP, _F, _F, _I, _VP, _VP, _VP, _VP, _VP]
+    lib.cimq_qconv_sizes.restype = ctypes.c_int
+    lib.cimq_qconv_sizes.argtypes = [ctypes.POINTER(QConvDesc), ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.POINTER(ctypes.c_size_t)]
+    lib.cimq_qconv_forward.restype = ctypes.c_int
+    lib.cimq_qconv_forward.argtypes = [ctypes.POINTER(QConvDesc)] + [_VP] * 9
+    lib.cimq_qconv_backward_scales.restype = ctypes.c_int
+    lib.cimq_qconv_backward_scales.argtypes = [ctypes.POINTER(QConvDesc)] + [_VP] * 8
     lib.cimq_profile_start.restype = ctypes.c_int
     lib.cimq_profile_start.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.cimq_profile_stop.restype = ctypes.c_int
@@ -185,6 +220,26 @@ def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha, flags=0) -> LsqDe
     q.nbits_alpha = int(nbits_alpha)
     q.flags = int(flags)
     return q
+
+
+def make_qconv_desc(B, C, H, W, O, KH, KW, stride, padding, dilation, groups, code_min, code_max,
+                    has_bias) -> QConvDesc:
+    d = QConvDesc()
+    d.batch, d.in_channels, d.in_h, d.in_w = int(B), int(C), int(H), int(W)
+    d.out_channels, d.kernel_h, d.kernel_w = int(O), int(KH), int(KW)
+    d.stride_h, d.stride_w = int(stride[0]), int(stride[1])
+    d.pad_h, d.pad_w = int(padding[0]), int(padding[1])
+    d.dilation_h, d.dilation_w = int(dilation[0]), int(dilation[1])
+    d.groups = int(groups)
+    d.code_min, d.code_max = int(code_min), int(code_max)
+    d.has_bias = 1 if has_bias else 0
+    return d
+
+
+def qconv_sizes(desc: QConvDesc):
+    f, b = ctypes.c_size_t(), ctypes.c_size_t()
+    check(load().cimq_qconv_sizes(ctypes.byref(desc), ctypes.byref(f), ctypes.byref(b)), "cimq_qconv_sizes")
+    return f.value, b.value
 
 
 def query_sizes(desc: ConvDesc) -> Sizes:

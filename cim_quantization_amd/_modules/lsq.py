@@ -7,8 +7,8 @@ partial sums are integer MFMA products, the ADC is applied from exact integer th
 ``get_cim_output_signed`` is re-exported with the reference's 17-argument signature.
 
 ``Conv2dLSQ`` / ``LinearLSQ`` / ``ActLSQ`` (plain LSQ fake-quant, unused by the CiM
-example, SURVEY.md section 8f "next") are provided with the reference's semantics on
-torch device ops.
+example, SURVEY.md section 8f "next") run their quantisers on libcimq and Conv2dLSQ's conv of
+integer codes on int8 MFMA (functional.lsq_quantize / qconv2d).
 """
 from __future__ import annotations
 
@@ -18,7 +18,8 @@ import torch
 import torch.nn.functional as F
 
 from ..functional import (alpha_cim_init, cim_conv2d_lsq, cim_conv2d_lsq_shift, cim_module_conv,  # noqa: F401
-                          get_adcless_cim_output, get_analog_partial_sums_autograd_ver2, get_cim_output_signed)
+                          get_adcless_cim_output, get_analog_partial_sums_autograd_ver2, get_cim_output_signed,
+                          lsq_quantize, qconv2d)
 from ._quan_base import (_ActQ, _Conv2dQ, _Conv2dQCiM, _LinearQ, Qmodes, grad_scale,  # noqa: F401
                          round_pass)
 
@@ -141,7 +142,12 @@ class Conv2dLSQCiM(_Conv2dQCiM):
 
 
 class Conv2dLSQ(_Conv2dQ):
-    """Plain LSQ conv (lsq.py:389-436); consumes the (x_q, act_scale) tuple of ActLSQ."""
+    """Plain LSQ conv (lsq.py:389-436); consumes the (x_q, act_scale) tuple of ActLSQ.
+
+    The weight quantiser runs on libcimq (lsq_quantize) and the conv of the two integer-code
+    tensors on int8 MFMA (qconv2d) when x_q comes from this package's ActLSQ (codes by
+    construction, their range recorded on the tensor); any other x_q -- the reference accepts
+    arbitrary tensors in the tuple -- is convolved by torch's fp32 conv."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
                  groups=1, bias=True, nbits_w=8, **kwargs):
@@ -158,13 +164,18 @@ class Conv2dLSQ(_Conv2dQ):
             self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
             self.init_state.fill_(1)
         ws = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
-        w_q = round_pass((self.weight / ws).clamp(qn, qp))
+        w_q = lsq_quantize(self.weight, ws, qn, qp)
+        code_range = getattr(x_q, "_cimq_code_range", None)
+        if code_range is not None and self.groups == 1 and self.nbits <= 8:
+            return qconv2d(x_q, act_scale, w_q, ws, self.bias, self.stride, self.padding, self.dilation,
+                           code_range)
         y = F.conv2d(x_q, w_q, self.bias, self.stride, self.padding, self.dilation, self.groups)
         return y * act_scale * ws
 
 
 class LinearLSQ(_LinearQ):
-    """Plain LSQ linear (lsq.py:591-617)."""
+    """Plain LSQ linear (lsq.py:591-617): the weight quantiser on libcimq, the fp32 linear of the
+    unquantised input by torch's GEMM (the reference quantises only the weight here)."""
 
     def __init__(self, in_features, out_features, bias=True, nbits_w=4, **kwargs):
         super().__init__(in_features=in_features, out_features=out_features, bias=bias, nbits=nbits_w)
@@ -177,11 +188,12 @@ class LinearLSQ(_LinearQ):
             self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
             self.init_state.fill_(1)
         a = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
-        return F.linear(x, round_pass((self.weight / a).clamp(qn, qp)) * a, self.bias)
+        return F.linear(x, lsq_quantize(self.weight, a, qn, qp, scaled=True), self.bias)
 
 
 class ActLSQ(_ActQ):
-    """LSQ activation quantiser (lsq.py:620-662): returns (integer codes, step size)."""
+    """LSQ activation quantiser (lsq.py:620-662): returns (integer codes, step size); the codes
+    come from libcimq and carry their range for Conv2dLSQ's int8 conv."""
 
     def __init__(self, nbits_a=4, **kwargs):
         super().__init__(nbits=nbits_a)
@@ -202,4 +214,7 @@ class ActLSQ(_ActQ):
             self.init_state.fill_(1)
         qn, qp = self._range()
         a = grad_scale(self.alpha, 1.0 / math.sqrt(x.numel() * qp))
-        return round_pass((x / a).clamp(qn, qp)), a
+        x_q = lsq_quantize(x, a, qn, qp)
+        if -128 <= qn and qp <= 255 and (qn >= 0 or qp <= 127):
+            x_q._cimq_code_range = (int(qn), int(qp))
+        return x_q, a

@@ -570,3 +570,109 @@ def logical_macs(B, C, H, W, O, KH, KW, stride, padding) -> int:
 
 def num_xbars(in_channels, kernel_size, xbar) -> int:
     return int(math.ceil(in_channels * kernel_size[0] * kernel_size[1] / xbar))
+
+
+# =============================================================================================
+# plain LSQ modules (lsq.py:389-436 Conv2dLSQ, :591-617 LinearLSQ, :620-662 ActLSQ)
+# =============================================================================================
+class _LsqQuantize(torch.autograd.Function):
+    """out = round_pass(clamp(x / s, qn, qp)) [* s] with s the grad-scaled step size (a [1]
+    tensor: grad_scale(alpha, g) evaluated by torch, so its graph back to alpha stays torch's).
+    Backward: grad_x and d loss / d s from libcimq (cimq_lsq_quantize_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, s, qn, qp, scaled):
+        _require_device(x, s)
+        xc = x.detach().float().contiguous()
+        sc = s.detach().float().reshape(-1)[:1].contiguous()
+        out = torch.empty_like(xc)
+        _lib.check(_lib.load().cimq_lsq_quantize_forward(xc.data_ptr(), xc.numel(), sc.data_ptr(), float(qn),
+                                                         float(qp), 1 if scaled else 0, out.data_ptr(), _stream()),
+                   "cimq_lsq_quantize_forward")
+        ctx.save_for_backward(xc, sc)
+        ctx.q = (float(qn), float(qp), 1 if scaled else 0)
+        ctx.s_shape = s.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, sc = ctx.saved_tensors
+        qn, qp, scaled = ctx.q
+        lib = _lib.load()
+        gc = g.float().contiguous()
+        gx = torch.empty_like(xc)
+        gs = torch.empty(1, device=xc.device, dtype=torch.float32)
+        ws = torch.empty(max(lib.cimq_lsq_quantize_workspace_bytes(xc.numel()), 4), device=xc.device,
+                         dtype=torch.uint8)
+        _lib.check(lib.cimq_lsq_quantize_backward(xc.data_ptr(), xc.numel(), sc.data_ptr(), qn, qp, scaled,
+                                                  gc.data_ptr(), gx.data_ptr(), gs.data_ptr(), ws.data_ptr(),
+                                                  _stream()), "cimq_lsq_quantize_backward")
+        return gx, gs.reshape(ctx.s_shape), None, None, None
+
+
+def lsq_quantize(x, s, qn, qp, scaled=False):
+    """LSQ fake-quantiser on libcimq: round_pass(clamp(x / s, qn, qp)) [* s] (lsq.py:412,611,656)."""
+    return _LsqQuantize.apply(x, s, qn, qp, scaled)
+
+
+class _QConv2d(torch.autograd.Function):
+    """Conv2dLSQ's quantised conv (lsq.py:436): conv2d(x_q, w_q, bias) * act_scale * w_scale with
+    integer-code operands, forward on int8 MFMA (cimq_qconv_forward).  Backward: the scale
+    products and grad_y0 on libcimq (cimq_qconv_backward_scales), the conv's input / weight
+    gradients of grad_y0 as plain fp32 convolutions (torch.nn.grad: the library conv)."""
+
+    @staticmethod
+    def forward(ctx, x_q, act_scale, w_q, w_scale, bias, stride, padding, dilation, code_range):
+        _require_device(x_q, act_scale, w_q, w_scale, bias)
+        xc = x_q.detach().float().contiguous()
+        wc = w_q.detach().float().contiguous()
+        a = act_scale.detach().float().reshape(-1)[:1].contiguous()
+        s = w_scale.detach().float().reshape(-1)[:1].contiguous()
+        bc = None if bias is None else bias.detach().float().contiguous()
+        B, C, H, W = xc.shape
+        O, _, KH, KW = wc.shape
+        desc = _lib.make_qconv_desc(B, C, H, W, O, KH, KW, stride, padding, dilation, 1, code_range[0],
+                                    code_range[1], bc is not None)
+        fws, bws = _lib.qconv_sizes(desc)
+        Ho = (H + 2 * padding[0] - dilation[0] * (KH - 1) - 1) // stride[0] + 1
+        Wo = (W + 2 * padding[1] - dilation[1] * (KW - 1) - 1) // stride[1] + 1
+        y = torch.empty(B, O, Ho, Wo, device=xc.device, dtype=torch.float32)
+        y0 = torch.empty_like(y)
+        ws = torch.empty(max(fws, 16), device=xc.device, dtype=torch.uint8)
+        _lib.check(_lib.load().cimq_qconv_forward(desc, xc.data_ptr(), wc.data_ptr(), a.data_ptr(), s.data_ptr(),
+                                                  None if bc is None else bc.data_ptr(), y.data_ptr(), y0.data_ptr(),
+                                                  ws.data_ptr(), _stream()), "cimq_qconv_forward")
+        ctx.save_for_backward(xc, wc, a, s, y0)
+        ctx.desc, ctx.bws = desc, bws
+        ctx.conv = (tuple(stride), tuple(padding), tuple(dilation))
+        ctx.shapes = (act_scale.shape, w_scale.shape, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, wc, a, s, y0 = ctx.saved_tensors
+        stride, padding, dilation = ctx.conv
+        gc = g.float().contiguous()
+        gy0 = torch.empty_like(y0)
+        scales = torch.empty(2, device=y0.device, dtype=torch.float32)
+        ws = torch.empty(max(ctx.bws, 16), device=y0.device, dtype=torch.uint8)
+        _lib.check(_lib.load().cimq_qconv_backward_scales(ctx.desc, gc.data_ptr(), y0.data_ptr(), a.data_ptr(),
+                                                          s.data_ptr(), gy0.data_ptr(), scales.data_ptr(),
+                                                          ws.data_ptr(), _stream()), "cimq_qconv_backward_scales")
+        a_shape, s_shape, has_bias = ctx.shapes
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(xc.shape, wc, gy0, stride, padding, dilation, 1)
+        if ctx.needs_input_grad[2]:
+            gw = torch.nn.grad.conv2d_weight(xc, wc.shape, gy0, stride, padding, dilation, 1)
+        gb = gy0.sum(dim=(0, 2, 3)) if has_bias else None
+        return gx, scales[1:2].reshape(a_shape), gw, scales[0:1].reshape(s_shape), gb, None, None, None, None
+
+
+def qconv2d(x_q, act_scale, w_q, w_scale, bias=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1),
+            code_range=(-128, 127)):
+    """conv2d(x_q, w_q, bias) * act_scale * w_scale on int8 MFMA; x_q / w_q hold integer codes,
+    x_q's within ``code_range`` (ActLSQ's [Qn, Qp]; [0, 255] runs as two 4-bit halves)."""
+    pair = lambda v: tuple(v) if isinstance(v, (tuple, list)) else (int(v), int(v))  # noqa: E731
+    return _QConv2d.apply(x_q, act_scale, w_q, w_scale, bias, pair(stride), pair(padding), pair(dilation),
+                          tuple(int(c) for c in code_range))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 4
+#define CIMQ_ABI_VERSION 5
 
 /* status codes */
 #define CIMQ_OK 0
@@ -211,6 +211,51 @@ int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float
  * CIMQ_EUNSUPPORTED for layers whose forward writes no state words. */
 int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* code_out, uint8_t* pass_out,
                            void* stream);
+
+/* ---- plain LSQ modules (lsq.py:389-436 Conv2dLSQ, :591-617 LinearLSQ, :620-662 ActLSQ) ---- */
+
+/* The LSQ quantiser out = round_pass(clamp(x / s, qn, qp)) [* s if scaled] over n fp32
+ * elements (x, out 16-byte aligned), s = *s the grad-scaled step size (grad_scale(alpha, g),
+ * lsq.py:407-412 / :608-611 / :653-656, evaluated by the caller).  Replaces those lines'
+ * torch ops: ActLSQ's codes (scaled = 0), Conv2dLSQ's weight codes (0), LinearLSQ's w_q (1). */
+int cimq_lsq_quantize_forward(const float* x, long long n, const float* s, float qn, float qp, int scaled,
+                              float* out, void* stream);
+
+/* Autograd of cimq_lsq_quantize_forward: grad_x (STE through round_pass, the clamp mask,
+ * DivBackward wrt x) and grad_s[1] = d loss / d s (MulBackward's sum when scaled, then
+ * DivBackward's -grad_t * ((x / s) / s)), reduced in a fixed order.  ``ws`` holds
+ * cimq_lsq_quantize_workspace_bytes(n). */
+size_t cimq_lsq_quantize_workspace_bytes(long long n);
+int cimq_lsq_quantize_backward(const float* x, long long n, const float* s, float qn, float qp, int scaled,
+                               const float* grad_out, float* grad_x, float* grad_s, void* ws, void* stream);
+
+/* Conv2dLSQ's conv of integer codes (lsq.py:436): x_codes [B,C,H,W] and w_codes [O,C,KH,KW]
+ * are fp32 tensors holding integers (ActLSQ / weight-quantiser codes) in [code_min, code_max]
+ * (activations) and [-128, 127] (weights). */
+typedef struct cimq_qconv_desc {
+  int32_t batch, in_channels, in_h, in_w;
+  int32_t out_channels, kernel_h, kernel_w;
+  int32_t stride_h, stride_w, pad_h, pad_w, dilation_h, dilation_w, groups; /* groups must be 1 */
+  int32_t code_min, code_max; /* activation code range: within [-128, 127] or [0, 255] */
+  int32_t has_bias;
+  int32_t reserved;
+} cimq_qconv_desc;
+
+int cimq_qconv_sizes(const cimq_qconv_desc* d, size_t* fwd_workspace_bytes, size_t* bwd_workspace_bytes);
+
+/* y0 = conv2d(x_codes, w_codes) (+ bias) on int8 MFMA (exact int32 sums, then fp32; the
+ * reference's fp32 conv of the same integers is exact while |sum| < 2^24) and
+ * y = (y0 * act_scale) * w_scale, both [B, O, Ho, Wo].  y0 is kept for the backward (the
+ * tensor torch's MulBackward saves).  act_scale / w_scale: device pointers to one float. */
+int cimq_qconv_forward(const cimq_qconv_desc* d, const float* x_codes, const float* w_codes, const float* act_scale,
+                       const float* w_scale, const float* bias, float* y, float* y0, void* ws, void* stream);
+
+/* Elementwise backward of y = (y0 * act_scale) * w_scale: grad_y0 = (grad_y * w_scale) * act_scale,
+ * grad_scales[0] = sum grad_y * (y0 * act_scale) (d / d w_scale), grad_scales[1] =
+ * sum (grad_y * w_scale) * y0 (d / d act_scale).  The conv's own input / weight gradients of
+ * grad_y0 are plain fp32 convolutions (the caller's library conv). */
+int cimq_qconv_backward_scales(const cimq_qconv_desc* d, const float* grad_y, const float* y0, const float* act_scale,
+                               const float* w_scale, float* grad_y0, float* grad_scales, void* ws, void* stream);
 
 /* Diagnostic kernel timer.  Until cimq_profile_stop(), every launch of kernel ``kernel_id``
  * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep, each over

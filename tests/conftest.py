@@ -59,3 +59,16 @@ def cuda_device():
 def shift_manifest():
     with open(os.path.join(GOLDEN, "manifest_shift.json")) as f:
         return json.load(f)
+
+
+def plain_manifest():
+    with open(os.path.join(GOLDEN, "manifest_plain.json")) as f:
+        return json.load(f)
+
+
+def normwise_err(mine, ref):
+    """max |mine - ref| / max |ref| (gradients of contractions, which cancel elementwise)."""
+    mine = np.asarray(mine, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert mine.shape == ref.shape, (mine.shape, ref.shape)
+    return float(np.abs(mine - ref).max() / (np.abs(ref).max() + 1e-30))

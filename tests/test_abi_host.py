@@ -21,7 +21,7 @@ def lib():
 def header_symbols():
     with open(os.path.join(REPO, "include", "cimq.h")) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cimq_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(cimq_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_and_binding_agree():
@@ -85,7 +85,7 @@ def header_arities():
     with open(os.path.join(REPO, "include", "cimq.h")) as f:
         txt = f.read()
     out = {}
-    for m in re.finditer(r"^\s*(?:int|const char\*)\s+(cimq_\w+)\s*\(([^)]*)\)\s*;", txt, re.M | re.S):
+    for m in re.finditer(r"^\s*(?:int|size_t|const char\*)\s+(cimq_\w+)\s*\(([^)]*)\)\s*;", txt, re.M | re.S):
         params = m.group(2).strip()
         out[m.group(1)] = 0 if params in ("", "void") else len(params.split(","))
     return out
