@@ -137,20 +137,46 @@ __global__ __launch_bounds__(256) void lsq_partials_finish_kernel(int nblk, cons
 
 // ---------------------------------------------------------------------------------------
 // int8 conv of integer codes (Conv2dLSQ, lsq.py:436): y0 = conv2d(x_q, w_q) (+ bias),
-// y = y0 * act_scale * w_scale.  Implicit GEMM: D[o][pixel] = sum_k W[o][k] X[k][pixel],
-// k = (c, kh, kw); A = packed weight codes (rows o), B = the lane's 16 gathered codes
-// (column = pixel), so a lane's four results are four channels of one pixel and each store
-// instruction writes 16 consecutive pixels of four channels (NCHW rows).
+// y = y0 * act_scale * w_scale.  Implicit GEMM D[o][pixel] = sum_k W[o][k] X[k][pixel] with
+// the contraction ordered k = (kh, kw, c), channels fastest (integer sums: any order is exact):
+// a pre-pass writes the codes as int8 NHWC with channels padded to 16, so one lane's 16
+// consecutive k -- 16 channels of one tap -- are ONE 16-byte load.  A = packed weight codes
+// (rows o), B = those loads (column = pixel): a lane's four results are four channels of one
+// pixel and each store instruction writes 16 consecutive pixels of four channels (NCHW rows).
 // ---------------------------------------------------------------------------------------
 struct QConv {
   int B, C, H, W, O, KH, KW, SH, SW, PH, PW, DH, DW, Ho, Wo;
-  int K, KS, NOB;  // contraction C*KH*KW, its 64-steps, 16-channel output blocks
+  int Cp;          // channels padded to 16
+  int K, KS, NOB;  // contraction KH*KW*Cp, its 64-steps, 16-channel output blocks
   long long M;     // B*Ho*Wo
   int has_bias;
 };
 
+// xq8[((b*H + h)*W + w)*Cp + c] = int8 code (0 past C); one thread per 16 channels of a pixel
+__global__ __launch_bounds__(256) void qconv_nhwc_kernel(QConv q, const float* __restrict__ x,
+                                                         uint4* __restrict__ xq8) {
+  const int g16 = q.Cp >> 4;
+  const long long total = (long long)q.B * q.H * q.W * g16;
+  const long long HW = (long long)q.H * q.W;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(t % g16);
+    const long long pix = t / g16;  // b*H*W + h*W + w
+    const long long b = pix / HW, hw = pix - b * HW;
+    uint32_t wd[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int c = cg * 16 + e;
+      int v = 0;
+      if (c < q.C) v = __float2int_rn(x[((size_t)b * q.C + c) * HW + hw]);
+      wd[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
+    }
+    xq8[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+  }
+}
+
 // wpk[(ks * NOB + ob) * 64 + lane]: 16 int8 codes, row o = ob*16 + (lane & 15),
-// k = ks*64 + 16*(lane >> 4) + e; zero past K / O
+// k = ks*64 + 16*(lane >> 4) + e = (kh*KW + kw)*Cp + c; zero past C / the taps / O
 __global__ void qconv_pack_w_kernel(QConv q, const float* __restrict__ w, v4i* __restrict__ wpk) {
   const int total = q.KS * q.NOB * 64;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
@@ -161,8 +187,12 @@ __global__ void qconv_pack_w_kernel(QConv q, const float* __restrict__ w, v4i* _
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int k = ks * 64 + 16 * (lane >> 4) + e;
+      const int tap = k / q.Cp, c = k - tap * q.Cp;
       int v = 0;
-      if (o < q.O && k < q.K) v = __float2int_rn(w[(size_t)o * q.K + k]);
+      if (o < q.O && c < q.C && tap < q.KH * q.KW) {
+        const int kh = tap / q.KW, kw = tap - kh * q.KW;
+        v = __float2int_rn(w[(((size_t)o * q.C + c) * q.KH + kh) * q.KW + kw]);
+      }
       wd[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
     }
     wpk[t] = v4i{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
@@ -171,21 +201,10 @@ __global__ void qconv_pack_w_kernel(QConv q, const float* __restrict__ w, v4i* _
 
 // SPLIT: codes in [0, 255] (unsigned 8-bit activations) go through two MFMAs, x = 16 hi + lo
 template <int NB, bool SPLIT>
-__global__ __launch_bounds__(256) void qconv_fwd_kernel(QConv q, const float* __restrict__ x,
+__global__ __launch_bounds__(256) void qconv_fwd_kernel(QConv q, const uint4* __restrict__ xq8,
                                                         const v4i* __restrict__ wpk, const float* __restrict__ sa_p,
                                                         const float* __restrict__ sw_p, const float* __restrict__ bias,
                                                         float* __restrict__ y, float* __restrict__ y0) {
-  extern __shared__ int ktab[];  // k -> c << 16 | kh << 8 | kw, or -1 past K
-  for (int k = threadIdx.x; k < q.KS * 64; k += blockDim.x) {
-    int t = -1;
-    if (k < q.K) {
-      const int khw = q.KH * q.KW;
-      const int c = k / khw, rem = k - c * khw, kh = rem / q.KW, kw = rem - kh * q.KW;
-      t = (c << 16) | (kh << 8) | kw;
-    }
-    ktab[k] = t;
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const long long p = (long long)blockIdx.x * 64 + wave * 16 + r16;  // this lane's pixel (B column)
@@ -195,7 +214,8 @@ __global__ __launch_bounds__(256) void qconv_fwd_kernel(QConv q, const float* __
   const int pimg = valid ? (int)(p - (long long)b * P) : 0;
   const int oh = pimg / q.Wo, ow = pimg - oh * q.Wo;
   const int ih0 = oh * q.SH - q.PH, iw0 = ow * q.SW - q.PW;
-  const float* xb = x + (size_t)b * q.C * q.H * q.W;
+  const int g16 = q.Cp >> 4, ntap = q.KH * q.KW;
+  const uint4* xb = xq8 + (size_t)b * q.H * q.W * g16;
   const int ob0 = blockIdx.y * NB;
   v4i acc[NB], acch[NB];
 #pragma unroll
@@ -204,25 +224,23 @@ __global__ __launch_bounds__(256) void qconv_fwd_kernel(QConv q, const float* __
     acch[nb] = v4i{0, 0, 0, 0};
   }
   for (int ks = 0; ks < q.KS; ++ks) {
-    uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int t = ktab[ks * 64 + 16 * g4 + e];
-      int v = 0;
-      if (t >= 0 && valid) {
-        const int c = t >> 16, kh = (t >> 8) & 255, kw = t & 255;
-        const int ih = ih0 + kh * q.DH, iw = iw0 + kw * q.DW;
-        if (ih >= 0 && ih < q.H && iw >= 0 && iw < q.W) v = __float2int_rn(xb[((size_t)c * q.H + ih) * q.W + iw]);
-      }
-      if (SPLIT) {
-        lo[e >> 2] |= (uint32_t)(v & 15) << (8 * (e & 3));
-        hi[e >> 2] |= (uint32_t)((v >> 4) & 15) << (8 * (e & 3));
-      } else {
-        lo[e >> 2] |= ((uint32_t)(uint8_t)(int8_t)v) << (8 * (e & 3));
-      }
+    const int kc = ks * 4 + g4;  // this lane's 16-channel chunk of the contraction
+    const int tap = kc / g16, cg = kc - tap * g16;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (tap < ntap && valid) {
+      const int kh = tap / q.KW, kw = tap - kh * q.KW;
+      const int ih = ih0 + kh * q.DH, iw = iw0 + kw * q.DW;
+      if (ih >= 0 && ih < q.H && iw >= 0 && iw < q.W) v = xb[((size_t)ih * q.W + iw) * g16 + cg];
     }
-    const v4i bl = v4i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]};
-    const v4i bh = v4i{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    v4i bl, bh;
+    if (SPLIT) {
+      bl = v4i{(int)(v.x & 0x0F0F0F0Fu), (int)(v.y & 0x0F0F0F0Fu), (int)(v.z & 0x0F0F0F0Fu), (int)(v.w & 0x0F0F0F0Fu)};
+      bh = v4i{(int)((v.x >> 4) & 0x0F0F0F0Fu), (int)((v.y >> 4) & 0x0F0F0F0Fu), (int)((v.z >> 4) & 0x0F0F0F0Fu),
+               (int)((v.w >> 4) & 0x0F0F0F0Fu)};
+    } else {
+      bl = v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      bh = bl;
+    }
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       if (ob0 + nb < q.NOB) {
@@ -277,6 +295,8 @@ inline int ew_blocks(long long n) { return (int)std::max(1LL, std::min<long long
 
 using namespace cimq;
 
+static size_t qconv_xq8_offset(const QConv& q) { return align256((size_t)q.KS * q.NOB * 64 * 16); }
+
 static int qconv_geo(const cimq_qconv_desc* d, QConv* q) {
   if (!d) return fail(CIMQ_EINVAL, "null qconv descriptor");
   QConv g;
@@ -294,12 +314,12 @@ static int qconv_geo(const cimq_qconv_desc* d, QConv* q) {
   g.Ho = (g.H + 2 * g.PH - g.DH * (g.KH - 1) - 1) / g.SH + 1;
   g.Wo = (g.W + 2 * g.PW - g.DW * (g.KW - 1) - 1) / g.SW + 1;
   if (g.Ho < 1 || g.Wo < 1) return fail(CIMQ_EINVAL, "qconv: empty output");
-  g.K = g.C * g.KH * g.KW;
+  g.Cp = (g.C + 15) / 16 * 16;
+  g.K = g.KH * g.KW * g.Cp;
   g.KS = (g.K + 63) / 64;
   g.NOB = (g.O + 15) / 16;
   g.M = (long long)g.B * g.Ho * g.Wo;
   g.has_bias = d->has_bias ? 1 : 0;
-  if ((size_t)g.KS * 64 * 4 > 60000) return fail(CIMQ_EUNSUPPORTED, "qconv: contraction too long (K > 15000)");
   *q = g;
   return CIMQ_OK;
 }
@@ -338,7 +358,7 @@ int cimq_lsq_quantize_backward(const float* x, long long n, const float* s, floa
 int cimq_qconv_sizes(const cimq_qconv_desc* d, size_t* fwd_workspace_bytes, size_t* bwd_workspace_bytes) {
   QConv q;
   CIMQ_TRY(qconv_geo(d, &q));
-  if (fwd_workspace_bytes) *fwd_workspace_bytes = (size_t)q.KS * q.NOB * 64 * 16;
+  if (fwd_workspace_bytes) *fwd_workspace_bytes = qconv_xq8_offset(q) + (size_t)q.B * q.H * q.W * q.Cp;
   if (bwd_workspace_bytes) *bwd_workspace_bytes = (size_t)2 * sizeof(float) * ew_blocks(q.M * q.O);
   return CIMQ_OK;
 }
@@ -354,13 +374,16 @@ int cimq_qconv_forward(const cimq_qconv_desc* d, const float* x_codes, const flo
   const int npk = q.KS * q.NOB * 64;
   hipLaunchKernelGGL(qconv_pack_w_kernel, dim3((npk + 255) / 256), dim3(256), 0, st, q, w_codes, wpk);
   CIMQ_TRY(check_hip("qconv_pack_w"));
+  uint4* xq8 = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(ws) + qconv_xq8_offset(q));
+  const long long nx = (long long)q.B * q.H * q.W * (q.Cp / 16);
+  hipLaunchKernelGGL(qconv_nhwc_kernel, dim3((unsigned)std::min<long long>((nx + 255) / 256, 65536)), dim3(256), 0, st,
+                     q, x_codes, xq8);
+  CIMQ_TRY(check_hip("qconv_nhwc"));
   const bool split = d->code_max > 127;
   const int NB = q.NOB >= 4 ? 4 : (q.NOB >= 2 ? 2 : 1);
   dim3 grid((unsigned)((q.M + 63) / 64), (unsigned)((q.NOB + NB - 1) / NB));
-  const size_t lds = (size_t)q.KS * 64 * 4;
   auto launch = [&](auto kern) {
-    CIMQ_TRY(set_lds(kern, lds));
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, x_codes, wpk, act_scale, w_scale, bias, y, y0);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, q, xq8, wpk, act_scale, w_scale, bias, y, y0);
     return check_hip("qconv_fwd");
   };
   if (NB == 4) return split ? launch(qconv_fwd_kernel<4, true>) : launch(qconv_fwd_kernel<4, false>);
