@@ -302,6 +302,63 @@ def bench_cfg5(dev, steps, warmup):
             "fwd_mac_per_s": macs / fw, "fwd_bwd_mac_per_s": macs / fb, "launch": "eager"}
 
 
+def resnet56_convs():
+    """(name, in, out, H, stride, bits) of ResNet-56's 55 CiM convs (models/cifar10/resnet.py, 9 blocks
+    per stage; the first conv forced to w8a8 by ReplaceModuleTool)."""
+    convs = [("conv1", 3, 16, 32, 1, 8)]
+    for st, (cin, cout, h) in enumerate(((16, 16, 32), (16, 32, 32), (32, 64, 16))):
+        for b in range(9):
+            s = 2 if (st > 0 and b == 0) else 1
+            c_in = cin if b == 0 else cout
+            h_in = h if b == 0 else (h // 2 if st > 0 else h)
+            convs.append((f"layer{st + 1}.{b}.conv1", c_in, cout, h_in, s, 2))
+            convs.append((f"layer{st + 1}.{b}.conv2", cout, cout, out_hw(h_in, s), 1, 2))
+    return convs
+
+
+def bench_layers(dev, specs, batch, xbar, adc, steps, warmup, adc_shift=False, ref=None):
+    """fwd+bwd and fwd-only wall time of a stack of Conv2dLSQCiM layers (eager launches; the
+    first-step alpha init runs in the warm-up), logical MAC/s as SURVEY 8(d) defines it."""
+    import cim_quantization_amd._modules as my_nn
+    torch.manual_seed(11)
+    layers, xs, gs, macs = [], [], [], 0
+    for name, c, o, h, s, nb in specs:
+        m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
+                               abitslice=1, xbar=xbar, adcbits=adc, adc_shift=adc_shift)
+        torch.nn.init.kaiming_normal_(m.weight)
+        layers.append(m.to(dev).train())
+        x = torch.randn(batch, c, h, h, device=dev)
+        xs.append(x if name == "conv1" else x.relu())
+        ho = out_hw(h, s)
+        gs.append(torch.randn(batch, o, ho, ho, device=dev) / math.sqrt(batch * o * ho * ho))
+        macs += batch * ho * ho * o * c * 9
+
+    def fb():
+        for m, x, g in zip(layers, xs, gs):
+            m(x).backward(g)
+
+    for _ in range(max(1, warmup)):
+        fb()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fb()
+    torch.cuda.synchronize(dev)
+    t_fb = (time.perf_counter() - t0) / steps
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            for m, x in zip(layers, xs):
+                m(x)
+        torch.cuda.synchronize(dev)
+    t_f = (time.perf_counter() - t0) / steps
+    out = {"ms_fwd_bwd": t_fb * 1e3, "ms_fwd": t_f * 1e3, "fwd_mac_per_s": macs / t_f, "launch": "eager",
+           "layers": len(specs), "batch": batch}
+    if ref is not None:
+        out["reference_cpu_container_ms"] = ref
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -415,7 +472,21 @@ def main():
         "layer_fwd_bwd_ms": breakdown,
     }
     if world == 1 and not args.no_cfg5:
-        result["extra_configs"] = {"cfg5": bench_cfg5(dev, args.steps, args.warmup)}
+        ex = {"cfg5": bench_cfg5(dev, args.steps, args.warmup)}
+        one = [("layer", 16, 16, 32, 1, 3)]
+        # BASELINE.md's in-container reference times (8 Xeon cores) beside each extra config
+        ex["cfg1_adc4"] = dict(workload="conv3x3_16x16_32x32_w3a3_xbar64_adc4_b4",
+                               **bench_layers(dev, one, 4, 64, 4, args.steps, args.warmup,
+                                              ref={"fwd": 5.2, "fwd_bwd": 15.8}))
+        ex["cfg1_adc1.5"] = dict(workload="conv3x3_16x16_32x32_w3a3_xbar64_adc1.5_b4",
+                                 **bench_layers(dev, one, 4, 64, 1.5, args.steps, args.warmup,
+                                                ref={"fwd": 6.9, "fwd_bwd": 24.1}))
+        r56 = resnet56_convs()
+        ex["cfg4_alpha"] = dict(workload="resnet56_w2a2_xbar64_adc1.5_b256_55convs_alpha_only",
+                                **bench_layers(dev, r56, 256, 64, 1.5, 3, 1, ref={"fwd": 16890.0, "fwd_bwd": 50010.0}))
+        ex["cfg4_shift"] = dict(workload="resnet56_w2a2_xbar64_adc1.5_b256_55convs_alpha_beta_shift",
+                                **bench_layers(dev, r56, 256, 64, 1.5, 2, 1, adc_shift=True))
+        result["extra_configs"] = ex
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_batch, min(16, os.cpu_count() or 1))
     if rank == 0:
