@@ -100,9 +100,13 @@ class Trainer:
         self.bucket_mb = self.bucket.nbytes / 1e6
 
     def compute(self, xs, gs):
-        """fwd + bwd of every layer; gradients accumulate into the flat bucket."""
-        for m, x, gy in zip(self.layers, xs, gs):
-            m(x).backward(gy)
+        """fwd + bwd of every layer; gradients accumulate into the flat bucket.  Each layer's
+        parameter-gradient epilogue rides in the next layer's backward kernels (the chained module
+        backward, functional.chained_epilogues); the last one is flushed at the scope's end."""
+        from cim_quantization_amd.functional import chained_epilogues
+        with chained_epilogues():
+            for m, x, gy in zip(self.layers, xs, gs):
+                m(x).backward(gy)
         self.bucket.join()  # the parameter-gradient epilogues are part of the step
 
     def finish(self):

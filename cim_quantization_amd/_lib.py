@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -37,6 +37,8 @@ EXPORTED_SYMBOLS = (
     "cimq_module_forward",
     "cimq_module_backward",
     "cimq_module_backward_tail",
+    "cimq_module_backward_chain",
+    "cimq_pending_flush",
     "cimq_alpha_init",
     "cimq_shift_forward",
     "cimq_shift_backward",
@@ -104,6 +106,12 @@ class QConvDesc(ctypes.Structure):
     ]
 
 
+class Pending(ctypes.Structure):
+    """Mirror of ``cimq_pending`` (opaque; zero-initialised by ctypes)."""
+
+    _fields_ = [("opaque", ctypes.c_uint64 * 128)]
+
+
 class Sizes(ctypes.Structure):
     """Mirror of ``cimq_sizes``."""
 
@@ -137,6 +145,11 @@ def _bind(lib):
     lib.cimq_module_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 16
     lib.cimq_module_backward_tail.restype = ctypes.c_int
     lib.cimq_module_backward_tail.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 9
+    lib.cimq_module_backward_chain.restype = ctypes.c_int
+    lib.cimq_module_backward_chain.argtypes = ([ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 15 +
+                                               [ctypes.POINTER(Pending), _VP])
+    lib.cimq_pending_flush.restype = ctypes.c_int
+    lib.cimq_pending_flush.argtypes = [ctypes.POINTER(Pending), _VP]
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
     lib.cimq_shift_forward.restype = ctypes.c_int

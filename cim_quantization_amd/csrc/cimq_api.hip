@@ -58,16 +58,26 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   return CIMQ_OK;
 }
 
+static Carry no_carry() {
+  Carry c;
+  memset(&c, 0, sizeof(c));
+  return c;
+}
+
+// carry: a previous layer's finish to run inside the v7 grad_x launch (struct Carry); only the v7
+// path can carry, so callers check v7_plan(g).ok before passing a non-empty one
 int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
-                     const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused) {
+                     const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused,
+                     const Carry& carry = no_carry()) {
   const Plan7 p7 = v7_plan(g);
   if (p7.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
-    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
-    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
-    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq);
+    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
   }
+  if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
   return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
 }
 
@@ -279,13 +289,14 @@ static int act_parts(const Geo& g) {
 }
 
 // the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes
-static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
-                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
-                       float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s) {
+static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
+                      const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
+                      float* grad_alpha_weight, float* grad_alpha_cim) {
   const bool has_alpha = la.nbits_alpha > 0;
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
-  ModuleTail a;
+  Carry j = no_carry();
+  ModuleTail& a = j.a;
   a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
   a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
   a.scal = reinterpret_cast<const float*>(c + L.lsq_scal);
@@ -305,11 +316,41 @@ static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const u
   a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
   a.napart = act_parts(g);
   a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
-  hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(a.nwb + a.nga), dim3(1024), 0, s, g, la, a);
-  CIMQ_TRY(check_hip("module_bwd_tail"));
-  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, la, a);
+  j.g = g;
+  j.q = la;
+  j.tail_blocks = a.nwb + a.nga;
+  j.finish = 1;
+  return j;
+}
+
+static int launch_tail(const Carry& j, hipStream_t s) {
+  hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(j.tail_blocks), dim3(1024), 0, s, j.g, j.q, j.a);
+  return check_hip("module_bwd_tail");
+}
+
+static int launch_finish(const Carry& j, hipStream_t s) {
+  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, j.q, j.a);
   return check_hip("module_bwd_finish");
 }
+
+static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
+                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
+                       float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s) {
+  const Carry j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                           grad_alpha_cim);
+  CIMQ_TRY(launch_tail(j, s));
+  return launch_finish(j, s);
+}
+
+// cimq_pending (caller-owned host memory): the epilogue a chained module backward left behind,
+// and which part of it has run
+struct Pending {
+  uint32_t magic;
+  int tail_done;
+  Carry job;
+};
+static_assert(sizeof(Pending) <= sizeof(cimq_pending), "cimq_pending too small");
+constexpr uint32_t kPendingMagic = 0x63696d70u;
 
 static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   if (!q) return fail(CIMQ_EINVAL, "null LSQ descriptor");
@@ -395,11 +436,20 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   return check_hip("bpo_to_nchw");
 }
 
-int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out, const float* x,
-                         const float* weight, const float* alpha_act, const float* alpha_weight,
-                         const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,
-                         const void* ctx, float* grad_x, float* grad_weight, float* grad_alpha_act,
-                         float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream) {
+static int pending_run(Pending* pd, hipStream_t s) {
+  if (pd->magic != kPendingMagic) return CIMQ_OK;
+  if (!pd->tail_done) CIMQ_TRY(launch_tail(pd->job, s));
+  CIMQ_TRY(launch_finish(pd->job, s));
+  pd->magic = 0;
+  return CIMQ_OK;
+}
+
+static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                                const float* x, const float* weight, const float* alpha_act,
+                                const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
+                                const float* signed_act, const void* ctx, float* grad_x, float* grad_weight,
+                                float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
+                                Pending* pend, void* stream) {
   Geo g;
   CIMQ_TRY(make_geo(d, &g));
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
@@ -434,8 +484,19 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
     CIMQ_TRY(check_hip("nchw_to_bpo"));
     gsrc = bpo;
   }
+  // chained: the previous layer's finish rides in this layer's v7 grad_x launch (block 0); other
+  // paths run it first on its own
+  Carry carry = no_carry();
+  if (pend && pend->magic == kPendingMagic) {
+    if (v7_plan(g).ok && pend->tail_done) {
+      carry = pend->job;
+      pend->magic = 0;
+    } else {
+      CIMQ_TRY(pending_run(pend, s));
+    }
+  }
   bool lsq_fused = false;
-  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused));
+  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused, carry));
   // the act-LSQ partials: fused into the fast grad_x kernel, a separate pass otherwise
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
@@ -450,9 +511,52 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
     nparts = grid;
   }
   if (nparts != act_parts(g)) return fail(CIMQ_EINVAL, "internal: act-LSQ partial count mismatch");
+  if (pend) {
+    // the slab reductions run now (as extra 256-thread blocks of the next layer's grad_x they
+    // measured slower: each takes 4x the serial loads of a 1024-thread tail block); the
+    // one-block finish waits for the next chained call's grad_x or cimq_pending_flush
+    pend->job = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                         grad_alpha_cim);
+    CIMQ_TRY(launch_tail(pend->job, s));
+    pend->tail_done = 1;
+    pend->magic = kPendingMagic;
+    return CIMQ_OK;
+  }
   if (q->flags & CIMQ_LSQ_SKIP_TAIL) return CIMQ_OK;  // the caller runs cimq_module_backward_tail
   return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
                      grad_alpha_cim, s);
+}
+
+int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out, const float* x,
+                         const float* weight, const float* alpha_act, const float* alpha_weight,
+                         const float* alpha_cim, const int8_t* binary_mask, const float* signed_act,
+                         const void* ctx, float* grad_x, float* grad_weight, float* grad_alpha_act,
+                         float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream) {
+  return module_backward_impl(d, q, grad_out, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act,
+                              ctx, grad_x, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim, ws,
+                              nullptr, stream);
+}
+
+int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                               const float* x, const float* weight, const float* alpha_act,
+                               const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
+                               const float* signed_act, const void* ctx, float* grad_x, float* grad_weight,
+                               float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
+                               cimq_pending* pending, void* stream) {
+  if (!pending) return fail(CIMQ_EINVAL, "null cimq_pending");
+  Pending* pd = reinterpret_cast<Pending*>(pending);
+  if (pd->magic != 0 && pd->magic != kPendingMagic) return fail(CIMQ_EINVAL, "cimq_pending not initialised (zero it)");
+  if (q && (q->flags & CIMQ_LSQ_SKIP_TAIL)) return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL with the chained backward");
+  return module_backward_impl(d, q, grad_out, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act,
+                              ctx, grad_x, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim, ws, pd,
+                              stream);
+}
+
+int cimq_pending_flush(cimq_pending* pending, void* stream) {
+  if (!pending) return fail(CIMQ_EINVAL, "null cimq_pending");
+  Pending* pd = reinterpret_cast<Pending*>(pending);
+  if (pd->magic != 0 && pd->magic != kPendingMagic) return fail(CIMQ_EINVAL, "cimq_pending not initialised (zero it)");
+  return pending_run(pd, reinterpret_cast<hipStream_t>(stream));
 }
 
 int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,

@@ -510,10 +510,12 @@ int launch_alpha_init_sums(const Geo& g, const uint8_t* ctx, const float* sw, co
 // cimq_part_v7_*.hip: the v7 backward (grad_x v8 + grad_w v7) for one slice-pair shape
 template <int NBW, int NBA>
 int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
-                const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq);
+                const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
+                const Carry& carry);
 #define CIMQ_V7_SIG(NBW, NBA)                                                                              \
   int launch_v7_n<NBW, NBA>(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa, \
-                            const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq)
+                            const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, \
+                            const Carry& carry)
 extern template CIMQ_V7_SIG(2, 2);
 extern template CIMQ_V7_SIG(3, 3);
 extern template CIMQ_V7_SIG(8, 8);

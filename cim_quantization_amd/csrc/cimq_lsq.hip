@@ -7,66 +7,9 @@
 // each value with the reference's fp32 op sequence, and their autograd backward with the
 // order in which torch's engine accumulates the contributions.
 #pragma once
-#include "cimq_device.h"
+#include "cimq_lsq_dev.h"
 
 namespace cimq {
-
-struct LsqArgs {
-  float qn_w, qp_w;      // weight clamp range
-  float gs_a, gs_w;      // grad_scale factors
-  int nbits_alpha;       // 0: no alpha_cim
-  int nalpha;            // numel(alpha_cim) = T*nbw*nba*O
-};
-
-// block-wide reductions: across the wave with lane shuffles, then across the (<= 16) waves
-// through LDS with one barrier.  red needs 4 * 16 floats.
-__device__ inline float nan_max(float a, float b) { return (a != a || b != b) ? (a + b) : fmaxf(a, b); }
-__device__ inline float nan_min(float a, float b) { return (a != a || b != b) ? (a + b) : fminf(a, b); }
-
-// (max, min) with torch.max / torch.min's NaN propagation
-__device__ inline float2 block_max_min(float mx, float mn, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mx = nan_max(mx, __shfl_xor(mx, o));
-    mn = nan_min(mn, __shfl_xor(mn, o));
-  }
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[2 * w] = mx;
-    red[2 * w + 1] = mn;
-  }
-  __syncthreads();
-  float2 r = make_float2(red[0], red[1]);
-  for (int i = 1; i < nw; ++i) {
-    r.x = nan_max(r.x, red[2 * i]);
-    r.y = nan_min(r.y, red[2 * i + 1]);
-  }
-  __syncthreads();
-  return r;
-}
-
-__device__ inline float4 block_sum4(float4 v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    v.x += __shfl_xor(v.x, o);
-    v.y += __shfl_xor(v.y, o);
-    v.z += __shfl_xor(v.z, o);
-    v.w += __shfl_xor(v.w, o);
-  }
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0) reinterpret_cast<float4*>(red)[w] = v;
-  __syncthreads();
-  float4 r = reinterpret_cast<const float4*>(red)[0];
-  for (int i = 1; i < nw; ++i) {
-    const float4 t = reinterpret_cast<const float4*>(red)[i];
-    r.x += t.x;
-    r.y += t.y;
-    r.z += t.z;
-    r.w += t.w;
-  }
-  __syncthreads();
-  return r;
-}
 
 // =========================================================================================
 // forward prologue of the module entry points: one launch does the activation quantiser and
@@ -170,258 +113,6 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
     else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);
     else if (t < e4) wcy_item(g, ws, a.ncpbt, a.wcy, t - e3);
     else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4);
-  }
-}
-
-// =========================================================================================
-// backward epilogue of the module entry points: two launches.  Blocks [0, nwb) reduce the
-// grad_w slabs and run the weight quantiser's backward; blocks [nwb, nwb + nga) reduce the
-// grad_alpha slabs into d loss / d alpha_q; then one block runs alpha_cim's quantiser
-// backward and the two step-size gradients.  With accum set, every parameter gradient is
-// added into its output buffer (torch's AccumulateGrad: grad = grad + new).
-// =========================================================================================
-struct ModuleTail {
-  const float* gw_slab;
-  const float* ga_slab;
-  const float* scal;
-  const float* weight;
-  const float* alpha_cim;
-  const float* apart;  // act-LSQ partials of the grad_x kernel
-  float* wpart;        // [2 * nwb] weight-LSQ partials
-  float* gaq;          // d loss / d alpha_q
-  float* grad_weight;
-  float* grad_alpha_act;
-  float* grad_alpha_w;
-  float* grad_alpha_cim;
-  Params pp;
-  float cgrad;  // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
-  int nchunks, nwb, nga, napart, accum;
-};
-
-// grad_w slab sum -> G = d loss / d w_q, then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
-//   grad_weight = mask * (G * sw) / sw; per block the partial sums of G * rp (MulBackward,
-//   d/d sw) and of -grad_t1 * ((w / sw) / sw) (DivBackward wrt the divisor) -> wpart[2*blk].
-__device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
-  const size_t rows = (size_t)g.T * g.FBT * 16;
-  const size_t nout = rows * g.Opad;
-  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
-  const int sub = threadIdx.x >> 6;
-  const float vsum = reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  float p_mul = 0.f, p_div = 0.f;
-  if (sub == 0 && idx < nout) {
-    const int o = (int)(idx % g.Opad);
-    const size_t row = idx / g.Opad;
-    const int i = (int)(row / (g.FBT * 16)), fl = (int)(row - (size_t)i * g.FBT * 16);
-    const int f = i * g.xbar + fl;
-    if (o < g.O && fl < g.xbar && f < g.K) {
-      const float sa = a.scal[0], sw = a.scal[1];
-      const float G = vsum * (sa / (float)g.nbw);  // d loss / d w_q (as reduce_gw_v3)
-      const size_t e = (size_t)o * g.K + f;
-      const float t1 = a.weight[e] / sw;
-      const float c = clamp_nan(t1, q.qn_w, q.qp_w);
-      const float rp = round_pass_value(c);
-      const float grad_rp = G * sw;
-      const bool pass = (t1 >= q.qn_w) && (t1 <= q.qp_w);
-      const float grad_t1 = pass ? grad_rp : 0.f;
-      const float gwv = grad_t1 / sw;
-      a.grad_weight[e] = a.accum ? a.grad_weight[e] + gwv : gwv;
-      p_mul = G * rp;
-      p_div = -grad_t1 * (t1 / sw);
-    }
-  }
-  // both partials live in the first wave only: a butterfly there, no block barriers
-  if (sub == 0) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      p_mul += __shfl_xor(p_mul, o);
-      p_div += __shfl_xor(p_div, o);
-    }
-    if (threadIdx.x == 0) {
-      a.wpart[2 * blk] = p_mul;
-      a.wpart[2 * blk + 1] = p_div;
-    }
-  }
-}
-
-__device__ inline void galpha_role(const Geo& g, const ModuleTail& a, int blk, float* red) {
-  const int nkj = g.nbw * g.nba;
-  const size_t nout = (size_t)g.T * nkj * g.Opad;
-  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
-  const float s = reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  if ((threadIdx.x >> 6) == 0 && idx < nout) {
-    const int o = (int)(idx % g.Opad);
-    const size_t qq = idx / g.Opad;  // (i, k, j)
-    if (o < g.O) {
-      const int kj = (int)(qq % nkj);
-      const int i = (int)(qq / nkj);
-      const int k = kj / g.nba, j = kj - k * g.nba;
-      a.gaq[(((size_t)i * g.nbw + k) * g.nba + j) * g.O + o] = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
-    }
-  }
-}
-
-// Backward of alpha_q = clamp(round_pass(a / scale), 1, qp) * scale, scale = (max - min) / N,
-// from G = d loss / d alpha_q, as torch's engine runs it: DivBackward wrt a, then the scale's
-// MulBackward / DivBackward sums -> (max - min) / N -> MinBackward, then MaxBackward, each
-// spread evenly over ties.
-__device__ inline void alpha_cim_bwd_block(const LsqArgs& q, const ModuleTail& a, float* red) {
-  const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
-  const float qp_al = (float)((1 << q.nbits_alpha) - 1);
-  const float N = (float)((1 << q.nbits_alpha) - 2);
-  const float* G = a.gaq;
-  float s_mul = 0.f, s_div = 0.f, cmax = 0.f, cmin = 0.f;
-  for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float v = a.alpha_cim[e];
-    const float t = v / scale;
-    const float rp = round_pass_value(t);
-    const float c = clamp_nan(rp, 1.f, qp_al);
-    const bool pass = (rp >= 1.f) && (rp <= qp_al);
-    const float gt = pass ? G[e] * scale : 0.f;
-    s_mul += G[e] * c;
-    s_div += -gt * (t / scale);
-    cmax += ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f;
-    cmin += ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f;
-  }
-  const float4 r = block_sum4(make_float4(s_mul, s_div, cmax, cmin), red);
-  s_mul = r.x;
-  s_div = r.y;
-  cmax = r.z;
-  cmin = r.w;
-  const float gscale = s_mul + s_div;  // d loss / d scale
-  const float gdiff = gscale / N;      // DivBackward of (max - min) / N
-  const float pmax = gdiff / cmax, pmin = -gdiff / cmin;
-  for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-    const float v = a.alpha_cim[e];
-    const float t = v / scale;
-    const float rp = round_pass_value(t);
-    const bool pass = (rp >= 1.f) && (rp <= qp_al);
-    const float gt = pass ? G[e] * scale : 0.f;
-    const bool ismin = (mn != mn) ? (v != v) : (v == mn);
-    const bool ismax = (mx != mx) ? (v != v) : (v == mx);
-    float r = gt / scale;          // DivBackward wrt a
-    r = r + (ismin ? pmin : 0.f);  // MinBackward reaches alpha_cim before MaxBackward
-    r = r + (ismax ? pmax : 0.f);
-    a.grad_alpha_cim[e] = a.accum ? a.grad_alpha_cim[e] + r : r;
-  }
-}
-
-// d loss / d alpha_weight = (sum G*rp + sum div-term) * gs_w  (GradScale's MulBackward);
-// d loss / d alpha_act = (sum of the act-LSQ partials) * gs_a.
-__device__ inline void lsq_finish_block(const LsqArgs& q, const ModuleTail& a, float* red) {
-  float m = 0.f, d = 0.f, s = 0.f;
-  for (int t = threadIdx.x; t < a.nwb; t += blockDim.x) {
-    m += a.wpart[2 * t];
-    d += a.wpart[2 * t + 1];
-  }
-  for (int t = threadIdx.x; t < a.napart; t += blockDim.x) s += a.apart[t];
-  const float4 r = block_sum4(make_float4(m, d, s, 0.f), red);
-  m = r.x;
-  d = r.y;
-  s = r.z;
-  if (threadIdx.x == 0) {
-    const float gw = (m + d) * q.gs_w;  // MulBackward's contribution reaches sw first, then DivBackward's
-    const float ga = s * q.gs_a;
-    a.grad_alpha_w[0] = a.accum ? a.grad_alpha_w[0] + gw : gw;
-    a.grad_alpha_act[0] = a.accum ? a.grad_alpha_act[0] + ga : ga;
-  }
-}
-
-// The epilogue's last step (module_bwd_finish_kernel): alpha_cim's quantiser backward and the
-// two step-size gradients from the partials module_bwd_tail_kernel left.  It is a chain of
-// dependent memory round trips, so with nalpha <= 8 * 1024 every load is issued up front
-// (alpha_cim, d loss / d alpha_q, the accumulated gradient, both partial sets), the two
-// reductions share one pass, and the second sweep runs from registers.  Same per-thread
-// order, same sums as the two-sweep form (alpha_cim_bwd_block + lsq_finish_block).
-template <int N>
-__device__ inline void block_sumn(float (&v)[N], float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], o);
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int i = 0; i < N; ++i) red[w * N + i] = v[i];
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = red[i];
-  for (int k = 1; k < nw; ++k)
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += red[k * N + i];
-  __syncthreads();
-}
-
-__device__ inline void module_finish_block(const LsqArgs& q, const ModuleTail& a, float* red) {
-  constexpr int PER = 8;
-  if (q.nbits_alpha > 0 && q.nalpha > PER * (int)blockDim.x) {  // large alpha_cim: two sweeps
-    alpha_cim_bwd_block(q, a, red);
-    lsq_finish_block(q, a, red);
-    return;
-  }
-  const bool has_a = q.nbits_alpha > 0;
-  float av[PER], gv[PER], old[PER];
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int e = threadIdx.x + u * (int)blockDim.x;
-    const bool in = has_a && e < q.nalpha;
-    av[u] = in ? a.alpha_cim[e] : 0.f;
-    gv[u] = in ? a.gaq[e] : 0.f;
-    old[u] = (in && a.accum) ? a.grad_alpha_cim[e] : 0.f;
-  }
-  float m = 0.f, d = 0.f, sp = 0.f;
-  for (int t = threadIdx.x; t < a.nwb; t += blockDim.x) {
-    m += a.wpart[2 * t];
-    d += a.wpart[2 * t + 1];
-  }
-  for (int t = threadIdx.x; t < a.napart; t += blockDim.x) sp += a.apart[t];
-  const float scale = has_a ? a.scal[2] : 1.f, mx = has_a ? a.scal[3] : 0.f, mn = has_a ? a.scal[4] : 0.f;
-  const float qp_al = (float)((1 << q.nbits_alpha) - 1);
-  const float N = (float)((1 << q.nbits_alpha) - 2);
-  float s_mul = 0.f, s_div = 0.f, cmax = 0.f, cmin = 0.f;
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int e = threadIdx.x + u * (int)blockDim.x;
-    if (has_a && e < q.nalpha) {  // as alpha_cim_bwd_block's first sweep
-      const float v = av[u];
-      const float t = v / scale;
-      const float rp = round_pass_value(t);
-      const float c = clamp_nan(rp, 1.f, qp_al);
-      const bool pass = (rp >= 1.f) && (rp <= qp_al);
-      const float gt = pass ? gv[u] * scale : 0.f;
-      s_mul += gv[u] * c;
-      s_div += -gt * (t / scale);
-      cmax += ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f;
-      cmin += ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f;
-    }
-  }
-  float r[8] = {s_mul, s_div, cmax, cmin, m, d, sp, 0.f};
-  block_sumn<8>(r, red);
-  if (has_a) {
-    const float gdiff = (r[0] + r[1]) / N;  // d loss / d scale, then DivBackward of (max - min) / N
-    const float pmax = gdiff / r[2], pmin = -gdiff / r[3];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = threadIdx.x + u * (int)blockDim.x;
-      if (e < q.nalpha) {
-        const float v = av[u];
-        const float t = v / scale;
-        const float rp = round_pass_value(t);
-        const bool pass = (rp >= 1.f) && (rp <= qp_al);
-        const float gt = pass ? gv[u] * scale : 0.f;
-        const bool ismin = (mn != mn) ? (v != v) : (v == mn);
-        const bool ismax = (mx != mx) ? (v != v) : (v == mx);
-        float rr = gt / scale;
-        rr = rr + (ismin ? pmin : 0.f);
-        rr = rr + (ismax ? pmax : 0.f);
-        a.grad_alpha_cim[e] = a.accum ? old[u] + rr : rr;
-      }
-    }
-  }
-  if (threadIdx.x == 0) {  // as lsq_finish_block
-    const float gw = (r[4] + r[5]) * q.gs_w;
-    const float ga = r[6] * q.gs_a;
-    a.grad_alpha_w[0] = a.accum ? a.grad_alpha_w[0] + gw : gw;
-    a.grad_alpha_act[0] = a.accum ? a.grad_alpha_act[0] + ga : ga;
   }
 }
 

@@ -16,6 +16,7 @@ Device-only: CPU tensors raise (there is no CPU fallback in the product path).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -343,6 +344,52 @@ def cim_conv2d_lsq_shift(x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act,
                                     dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar)
 
 
+class _ChainState:
+    """The chained module backward of one device (cimq_module_backward_chain): the epilogue the
+    last call left, the tensors it reads / writes (kept alive until it has been issued), the stream
+    of the chain, and whether the end-of-backward flush is queued or a chained_epilogues() scope
+    owns the flush."""
+
+    def __init__(self):
+        self.pending = _lib.Pending()
+        self.keep = None
+        self.stream = None
+        self.queued = False
+        self.scopes = 0
+
+    def flush(self):
+        if self.keep is not None:
+            _lib.check(_lib.load().cimq_pending_flush(self.pending, self.stream), "cimq_pending_flush")
+        self.keep = None
+        self.queued = False
+
+
+_CHAINS = {}
+CHAIN_EPILOGUES = True  # tests switch it off to compare against the unchained backward
+
+
+def _chain(dev):
+    return _CHAINS.setdefault(dev.index if dev.index is not None else torch.cuda.current_device(), _ChainState())
+
+
+@contextlib.contextmanager
+def chained_epilogues(device=None):
+    """Chain the parameter-gradient epilogues of Conv2dLSQCiM backwards across separate
+    ``backward()`` calls made inside this scope (e.g. one per layer, as bench.py does): each
+    layer's epilogue runs inside the next layer's backward kernels and the last one is flushed
+    when the scope ends.  Without a scope, a single backward pass chains its layers and flushes
+    at its end (a queued autograd callback).  Applies to the in-place accumulating backward
+    (GradBucket-owned layers); read the gradients only after the scope."""
+    ch = _chain(torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device))
+    ch.scopes += 1
+    try:
+        yield
+    finally:
+        ch.scopes -= 1
+        if ch.scopes == 0:
+            ch.flush()
+
+
 class _CimModuleConv(torch.autograd.Function):
     """A whole Conv2dLSQCiM layer after its first-step init (lsq.py:544-581): the activation,
     weight and alpha_cim quantisers run inside libcimq on the raw parameters (no torch ops,
@@ -439,6 +486,26 @@ class _CimModuleConv(torch.autograd.Function):
             gac = None if ac is None else torch.empty_like(ac)
         ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
         lib = _lib.load()
+        if targets is not None and side is None and CHAIN_EPILOGUES:
+            # chained: this layer's epilogue runs inside the next layer's backward kernels (or at the
+            # flush); the previous layer's runs inside ours
+            ch = _chain(dev)
+            stream = _stream()
+            if ch.keep is not None and ch.stream != stream:
+                ch.flush()
+            if ch.scopes == 0 and not ch.queued:
+                torch.autograd.Variable._execution_engine.queue_callback(ch.flush)
+                ch.queued = True
+            ch.stream = stream
+            _lib.check(lib.cimq_module_backward_chain(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
+                                                      aa.data_ptr(), aw.data_ptr(),
+                                                      None if ac is None else ac.data_ptr(), bm.data_ptr(),
+                                                      sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(), gw.data_ptr(),
+                                                      gaa.data_ptr(), gaw.data_ptr(),
+                                                      None if gac is None else gac.data_ptr(), ws.data_ptr(),
+                                                      ch.pending, stream), "cimq_module_backward_chain")
+            ch.keep = (ws, cbuf, wc, ac, gw, gaa, gaw, gac)
+            return (gx,) + (None,) * 19
         _lib.check(lib.cimq_module_backward(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
                                             aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),
                                             bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 5
+#define CIMQ_ABI_VERSION 6
 
 /* status codes */
 #define CIMQ_OK 0
@@ -169,6 +169,28 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
 int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
                               const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
                               float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
+
+/* Opaque, caller-owned host memory for cimq_module_backward_chain: zero-initialise it once. */
+typedef struct cimq_pending {
+  uint64_t opaque[128];
+} cimq_pending;
+
+/* cimq_module_backward for a chain of layers run back to back on ONE stream (a network's
+ * backward pass): the parameter-gradient epilogue of each call (module_bwd_tail / _finish) is
+ * not launched but left in ``pending``; the NEXT chained call runs it inside its own grad_x /
+ * grad_w kernels as extra workgroups (or on its own first, when that layer's backward is not the
+ * v7 path), and leaves its own.  cimq_pending_flush runs whatever is left.  The parameter
+ * gradients of a call are therefore complete only after the next chained call or the flush has
+ * been issued on the stream; every buffer the call used (ctx, ws, weight, alpha_cim, the four
+ * gradient buffers) must stay valid until then.  Same arguments as cimq_module_backward;
+ * CIMQ_LSQ_SKIP_TAIL is refused. */
+int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                               const float* x, const float* weight, const float* alpha_act,
+                               const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
+                               const float* signed_act, const void* ctx, float* grad_x, float* grad_weight,
+                               float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
+                               cimq_pending* pending, void* stream);
+int cimq_pending_flush(cimq_pending* pending, void* stream);
 
 /* First-step alpha_cim initialisation (lsq.py:557-563 with get_analog_partial_sums_signed,
  * lsq.py:35-87): alpha_init[1,T,nbw,nba,1,O] = 2*mean_{b,p}|ps*sw*sa| / sqrt(Qp_adc), zeros

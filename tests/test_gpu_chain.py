@@ -1,0 +1,112 @@
+"""GPU: the chained module backward (cimq_module_backward_chain): each layer's parameter-gradient
+epilogue runs inside the next layer's grad_x / grad_w kernels (or on its own before a non-v7
+layer, and at the flush).  The gradients must match the unchained backward: grad_x bit for bit
+(same kernels), the parameter gradients to fp32 reduction order (the carried slab reductions
+stride by the host kernel's block size)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (C, O, H, stride, bits): w8a8 first conv, w3a3 stride 1 / 2, a 16x16 layer, and a 12x12 one
+# (non-power-of-two width: the general backward, so the chain flushes before it)
+SPECS = [(3, 16, 32, 1, 8), (16, 16, 32, 1, 3), (16, 32, 32, 2, 3), (32, 32, 16, 1, 3), (32, 32, 12, 1, 3),
+         (32, 64, 16, 2, 3), (64, 64, 8, 1, 3)]
+
+
+def _stack(dev, seed=5):
+    import cim_quantization_amd._modules as my_nn
+    from cim_quantization_amd.dist import GradBucket
+    torch.manual_seed(seed)
+    layers = []
+    for c, o, h, s, nb in SPECS:
+        m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, xbar=128,
+                               adcbits=1.5)
+        torch.nn.init.kaiming_normal_(m.weight)
+        layers.append(m.to(dev).train())
+    bucket = GradBucket([p for m in layers for p in m.parameters()])
+    bucket.own(layers)
+    return layers, bucket
+
+
+def _data(dev, B=8, seed=9):
+    g = torch.Generator().manual_seed(seed)
+    xs, gs = [], []
+    for c, o, h, s, nb in SPECS:
+        x = torch.randn(B, c, h, h, generator=g)
+        xs.append((x if nb == 8 else x.relu()).to(dev))
+        ho = (h + 2 - 3) // s + 1
+        gs.append((torch.randn(B, o, ho, ho, generator=g) / (B * o * ho * ho) ** 0.5).to(dev))
+    return xs, gs
+
+
+def _step(layers, bucket, xs, gs, chained_scope):
+    from cim_quantization_amd.functional import chained_epilogues
+    grads_x = []
+    bucket.zero()
+    scope = chained_epilogues() if chained_scope else torch.enable_grad()
+    with scope:
+        for m, x, g in zip(layers, xs, gs):
+            xr = x.detach().requires_grad_(True)
+            m(xr).backward(g)
+            grads_x.append(xr.grad)
+    torch.cuda.synchronize()
+    return grads_x, bucket.flat.detach().clone()
+
+
+def test_chained_equals_unchained_per_layer_backwards(cuda_device):
+    import cim_quantization_amd.functional as F
+    la, ba = _stack(cuda_device)
+    lb, bb = _stack(cuda_device)
+    xs, gs = _data(cuda_device)
+    for layers, bucket in ((la, ba), (lb, bb)):  # first step: the alpha initialisation (torch path)
+        _step(layers, bucket, xs, gs, False)
+    xs2, gs2 = _data(cuda_device, seed=10)
+    F.CHAIN_EPILOGUES = False
+    try:
+        gx_ref, flat_ref = _step(lb, bb, xs2, gs2, False)
+    finally:
+        F.CHAIN_EPILOGUES = True
+    gx_ch, flat_ch = _step(la, ba, xs2, gs2, True)
+    for i, (a, b) in enumerate(zip(gx_ch, gx_ref)):
+        if SPECS[i][2] == 12:  # the general backward sums grad_x with LDS float atomics
+            assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item()
+        else:
+            assert torch.equal(a, b), i
+    err = (flat_ch - flat_ref).abs().max().item()
+    assert err <= 1e-6 * flat_ref.abs().max().item(), err
+    assert torch.isfinite(flat_ch).all()
+
+
+def test_chain_inside_one_backward_pass(cuda_device):
+    """one backward() through a sequential stack: the end-of-backward callback flushes"""
+    import cim_quantization_amd.functional as F
+    la, ba = _stack(cuda_device)
+    lb, bb = _stack(cuda_device)
+    specs = [(16, 16, 32, 1, 3), (16, 16, 32, 1, 3), (16, 16, 32, 1, 3)]
+    import cim_quantization_amd._modules as my_nn
+    from cim_quantization_amd.dist import GradBucket
+    nets = []
+    for seed in (1, 1):
+        torch.manual_seed(seed)
+        ms = [my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, xbar=128, adcbits=1.5)
+              .to(cuda_device).train() for c, o, h, s, nb in specs]
+        bk = GradBucket([p for m in ms for p in m.parameters()])
+        bk.own(ms)
+        nets.append((torch.nn.Sequential(ms[0], torch.nn.ReLU(), ms[1], torch.nn.ReLU(), ms[2]), bk))
+    x = torch.randn(8, 16, 32, 32, device=cuda_device).relu()
+    for net, bk in nets:  # initialising step
+        bk.zero()
+        net(x).square().mean().backward()
+    outs = []
+    for i, (net, bk) in enumerate(nets):
+        bk.zero()
+        F.CHAIN_EPILOGUES = i == 0
+        try:
+            net(x).square().mean().backward()
+        finally:
+            F.CHAIN_EPILOGUES = True
+        torch.cuda.synchronize()
+        outs.append(bk.flat.detach().clone())
+    err = (outs[0] - outs[1]).abs().max().item()
+    assert err <= 1e-6 * outs[1].abs().max().item(), err

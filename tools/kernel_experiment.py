@@ -38,6 +38,7 @@ VARIANTS = {
     "fwd_nogather": ["CIMQ_EXP_FWD_NOGATHER"],
     "prep_noact": ["CIMQ_EXP_PREP_NOACT"],
     "prep_nowt": ["CIMQ_EXP_PREP_NOWT"],
+    "prep_nowt_nocomp": ["CIMQ_EXP_PREP_NOWT", "CIMQ_EXP_PREP_NOCOMP"],
     "prep_nofrag": ["CIMQ_EXP_PREP_NOACT", "CIMQ_EXP_PREP_NOFRAG"],
     "prep_noparams": ["CIMQ_EXP_PREP_NOACT", "CIMQ_EXP_PREP_NOPARAMS"],
 }
