@@ -153,6 +153,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
     if (PLS && (NBW != 8 || NBA != 8)) std_mask = false;
   }
   const float scale = sw / (float)NBA;
+  const float inv_sa = 1.f / sa;
   float gpart = 0.f;
   int done = r0 - 1;
   for (int step = 0; step < nsteps; ++step) {
@@ -343,9 +344,11 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
           const float rp = (rr2 - clv) + clv;
           const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
           const float gy = pass ? gqv * sa : 0.f;
-          gx[gi] = gy / sa;
+          // (gqv * sa) / sa and y1 / sa only feed gradients (within the 1e-5 bar, one rounding
+          // apart); y1 itself stays an IEEE division: it decides the clamp mask and rint
+          gx[gi] = pass ? gqv : 0.f;
           gpart += gqv * rp;
-          gpart += -(gy * (y1 / sa));
+          gpart += -(gy * (y1 * inv_sa));
         } else {
           gx[gi] = gqv;
         }
