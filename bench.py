@@ -103,7 +103,9 @@ class Trainer:
         """fwd + bwd of every layer; gradients accumulate into the flat bucket.  Each layer's
         parameter-gradient epilogue rides in the next layer's backward kernels (the chained module
         backward, functional.chained_epilogues); the last one is flushed at the scope's end."""
-        from cim_quantization_amd.functional import chained_epilogues
+        from cim_quantization_amd.functional import chained_epilogues, prepare_weights
+        # the weight side of all 19 prologues in one launch, ahead of the forwards
+        prepare_weights(self.layers)
         with chained_epilogues():
             for m, x, gy in zip(self.layers, xs, gs):
                 m(x).backward(gy)

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "cimq_module_backward_tail",
     "cimq_module_backward_chain",
     "cimq_pending_flush",
+    "cimq_module_prepare",
     "cimq_alpha_init",
     "cimq_shift_forward",
     "cimq_shift_backward",
@@ -88,7 +89,7 @@ class LsqDesc(ctypes.Structure):
 
     _fields_ = [("qn_w", ctypes.c_float), ("qp_w", ctypes.c_float), ("gscale_a", ctypes.c_float),
                 ("gscale_w", ctypes.c_float), ("nbits_alpha", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("wprep", ctypes.c_void_p)]
 
 
 class QConvDesc(ctypes.Structure):
@@ -116,7 +117,15 @@ class Sizes(ctypes.Structure):
     """Mirror of ``cimq_sizes``."""
 
     _fields_ = [("ctx_bytes", ctypes.c_size_t), ("fwd_workspace_bytes", ctypes.c_size_t),
-                ("bwd_workspace_bytes", ctypes.c_size_t)]
+                ("bwd_workspace_bytes", ctypes.c_size_t), ("wprep_bytes", ctypes.c_size_t)]
+
+
+class PrepareItem(ctypes.Structure):
+    """Mirror of ``cimq_prepare_item``."""
+
+    _fields_ = [("desc", ctypes.POINTER(ConvDesc)), ("lsq", ctypes.POINTER(LsqDesc)),
+                ("weight", ctypes.c_void_p), ("alpha_act", ctypes.c_void_p), ("alpha_weight", ctypes.c_void_p),
+                ("alpha_cim", ctypes.c_void_p), ("binary_mask", ctypes.c_void_p), ("wprep", ctypes.c_void_p)]
 
 
 _VP = ctypes.c_void_p
@@ -150,6 +159,8 @@ def _bind(lib):
                                                [ctypes.POINTER(Pending), _VP])
     lib.cimq_pending_flush.restype = ctypes.c_int
     lib.cimq_pending_flush.argtypes = [ctypes.POINTER(Pending), _VP]
+    lib.cimq_module_prepare.restype = ctypes.c_int
+    lib.cimq_module_prepare.argtypes = [ctypes.c_int, ctypes.POINTER(PrepareItem), _VP]
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
     lib.cimq_shift_forward.restype = ctypes.c_int
@@ -226,12 +237,13 @@ def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w
     return d
 
 
-def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha, flags=0) -> LsqDesc:
+def make_lsq_desc(qn_w, qp_w, gscale_a, gscale_w, nbits_alpha, flags=0, wprep=None) -> LsqDesc:
     q = LsqDesc()
     q.qn_w, q.qp_w = float(qn_w), float(qp_w)
     q.gscale_a, q.gscale_w = float(gscale_a), float(gscale_w)
     q.nbits_alpha = int(nbits_alpha)
     q.flags = int(flags)
+    q.wprep = wprep
     return q
 
 

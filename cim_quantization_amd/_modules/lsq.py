@@ -69,6 +69,16 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         # AccumulateGrad kernels); set by dist.GradBucket.own(), which owns the exchange
         self.accumulate_grads_in_place = False
         self.tail_stream = None  # GradBucket.own(overlap=True): stream of the parameter-gradient epilogue
+        self._wprep = None        # functional.prepare_weights: the next forward's weight side, computed ahead
+        self._last_x_shape = None
+
+    def _fused_ready(self):
+        """True once the steady-state library path applies and an input shape is known
+        (prepare_weights needs both)."""
+        flags = self._init_flags()
+        return (self.fused and flags[0] and (flags[1] or self.alpha_cim is None) and self.adcbits != 0
+                and not self.adc_shift and not self.stochastic_quant and self._last_x_shape is not None
+                and self.weight.is_cuda)
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
@@ -96,13 +106,16 @@ class Conv2dLSQCiM(_Conv2dQCiM):
             self.binary_mask = self.binary_mask.to(x.device)
         if (self.fused and flags[0] and (flags[1] or self.alpha_cim is None) and self.adcbits != 0
                 and not self.adc_shift):
-            # steady state: the three quantisers and the CiM conv in one library call each way
+            # steady state: the three quantisers and the CiM conv in one library call each way (the
+            # weight side possibly prepared ahead by prepare_weights; taken once)
+            wprep, self._wprep = self._wprep, None
+            self._last_x_shape = tuple(x.shape)
             out = cim_module_conv(x, self.weight, self.alpha_act, self.alpha_weight, self.alpha_cim,
                                   self.binary_mask, self.signed_act, self.stride, self.padding, self.dilation,
                                   self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
                                   self.xbar, self.nbits_alpha, self.accumulate_grads_in_place,
                                   bool(self.stochastic_quant),
-                                  self.tail_stream if self.accumulate_grads_in_place else None)
+                                  self.tail_stream if self.accumulate_grads_in_place else None, wprep)
             if self.bias is not None:
                 out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
             return out

@@ -27,23 +27,23 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   {
     int total = g.T * g.KS * g.NBLK * 64;
     hipLaunchKernelGGL(prep_wfrag_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
-                       reinterpret_cast<v4i*>(ctx + L.wfrag));
+                       reinterpret_cast<v4i*>(wreg(g, ctx) + L.wfrag));
     CIMQ_TRY(check_hip("prep_wfrag"));
   }
   if (need_wgx) {
     int total = g.T * g.FBT * g.NKS * 64;
     hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
-                       reinterpret_cast<v4i*>(ctx + L.wgx));
+                       reinterpret_cast<v4i*>(wreg(g, ctx) + L.wgx));
     const int Cp = (g.C + 15) / 16 * 16;
     const int tw = g.T * g.KHW * Cp * g.NKS * 4;
     hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
-                       reinterpret_cast<uint4*>(ctx + L.wtc));
+                       reinterpret_cast<uint4*>(wreg(g, ctx) + L.wtc));
     CIMQ_TRY(check_hip("prep_wgx"));
     const Plan7 p7 = v7_plan(g);
     if (p7.ok) {
       const int tc = g.T * p7.v.NCPBT * g.NKS * 64;
       hipLaunchKernelGGL(prep_wcy_kernel, dim3(cdiv(tc, blk)), dim3(blk), 0, s, g, w_q, sw, p7.v.NCPBT,
-                         reinterpret_cast<v4i*>(ctx + L.wcy));
+                         reinterpret_cast<v4i*>(wreg(g, ctx) + L.wcy));
       CIMQ_TRY(check_hip("prep_wcy"));
     }
   }
@@ -115,6 +115,7 @@ int cimq_query_sizes(const cimq_conv_desc* d, cimq_sizes* out) {
   CIMQ_TRY(make_geo(d, &g));
   if (!out) return fail(CIMQ_EINVAL, "null output");
   out->ctx_bytes = ctx_layout(g).total;
+  out->wprep_bytes = ctx_layout(g).wbytes;
   WsLayout W = ws_layout(g);
   out->fwd_workspace_bytes = W.total;
   out->bwd_workspace_bytes = W.total;
@@ -299,7 +300,7 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   ModuleTail& a = j.a;
   a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
   a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
-  a.scal = reinterpret_cast<const float*>(c + L.lsq_scal);
+  a.scal = reinterpret_cast<const float*>(wreg(g, c) + L.lsq_scal);
   a.weight = weight;
   a.alpha_cim = alpha_cim;
   a.apart = reinterpret_cast<float*>(w + W.lsq_part);
@@ -369,17 +370,61 @@ static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   return CIMQ_OK;
 }
 
+// the module prologue's arguments: activation side into ctx c, weight side into wreg(g, c)
+static ModulePrep module_prep_args(const Geo& g, const float* x, const float* weight, const float* alpha_act,
+                                   const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
+                                   const float* signed_act, uint8_t* c, int* nwblk) {
+  CtxLayout L = ctx_layout(g);
+  uint8_t* wr = wreg(g, c);
+  const bool fast = v3_plan(g).ok;
+  const Plan7 p7 = v7_plan(g);
+  ModulePrep a;
+  memset(&a, 0, sizeof(a));
+  a.x = x;
+  a.alpha_act = alpha_act;
+  a.alpha_w = alpha_weight;
+  a.weight = weight;
+  a.alpha_cim = alpha_cim;
+  a.signed_act = signed_act;
+  a.bmask = binary_mask;
+  a.xcf = c ? c + L.xcode : nullptr;
+  a.xcb = c ? c + L.xhat : nullptr;
+  a.wfrag = reinterpret_cast<v4i*>(wr + L.wfrag);
+  a.wgx = reinterpret_cast<v4i*>(wr + L.wgx);
+  a.wtc = reinterpret_cast<uint4*>(wr + L.wtc);
+  a.wcy = reinterpret_cast<v4i*>(wr + L.wcy);
+  a.Cp = (g.C + 15) / 16 * 16;
+  a.pp = params_of(g, c);
+  a.scal = reinterpret_cast<float*>(wr + L.lsq_scal);
+  a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 4 * 256), act_blocks());
+  a.nwf = g.T * g.KS * g.NBLK * 64;
+  a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;                   // general grad_x operand
+  a.nwt = (fast && !p7.ok) ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // v5 / v6 grad_x operand
+  a.ncpbt = p7.ok ? p7.v.NCPBT : 1;
+  a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;              // v8 grad_x operand
+  a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
+  return a;
+}
+
+// the checks every module entry point shares; applies q->wprep
+static int module_geo(const cimq_conv_desc* d, const cimq_lsq_desc* q, Geo* g, LsqArgs* la) {
+  CIMQ_TRY(make_geo(d, g));
+  if (g->input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  if (g->variant == VAR_SHIFT_ROUND || g->variant == VAR_SHIFT_SIGN)
+    return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
+  CIMQ_TRY(lsq_args(*g, q, la));
+  g->wbase = reinterpret_cast<const unsigned char*>(q->wprep);
+  return CIMQ_OK;
+}
+
 int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
                         const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
                         const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
                         void* stream) {
   Geo g;
-  CIMQ_TRY(make_geo(d, &g));
-  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
-  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
-    return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
   LsqArgs la;
-  CIMQ_TRY(lsq_args(g, q, &la));
+  CIMQ_TRY(module_geo(d, q, &g, &la));
   if (!x || !weight || !alpha_act || !alpha_weight || !binary_mask || !signed_act || !out || !ctx || !ws)
     return fail(CIMQ_EINVAL, "null pointer argument");
   const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
@@ -388,35 +433,12 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   uint8_t* c = reinterpret_cast<uint8_t*>(ctx);
   CtxLayout L = ctx_layout(g);
-  float* scal = reinterpret_cast<float*>(c + L.lsq_scal);
+  float* scal = reinterpret_cast<float*>(wreg(g, c) + L.lsq_scal);
   {
-    const bool fast = v3_plan(g).ok;
-    ModulePrep a;
-    a.x = x;
-    a.alpha_act = alpha_act;
-    a.alpha_w = alpha_weight;
-    a.weight = weight;
-    a.alpha_cim = has_alpha ? alpha_cim : nullptr;
-    a.signed_act = signed_act;
-    a.bmask = binary_mask;
-    a.xcf = c + L.xcode;
-    a.xcb = c + L.xhat;
-    a.wfrag = reinterpret_cast<v4i*>(c + L.wfrag);
-    a.wgx = reinterpret_cast<v4i*>(c + L.wgx);
-    a.wtc = reinterpret_cast<uint4*>(c + L.wtc);
-    a.Cp = (g.C + 15) / 16 * 16;
-    a.pp = params_of(g, c);
-    a.scal = scal;
-    a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 4 * 256), act_blocks());
-    a.nwf = g.T * g.KS * g.NBLK * 64;
-    const Plan7 p7 = v7_plan(g);
-    a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;                   // general grad_x operand
-    a.nwt = (fast && !p7.ok) ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // v5 / v6 grad_x operand
-    a.wcy = reinterpret_cast<v4i*>(c + L.wcy);
-    a.ncpbt = p7.ok ? p7.v.NCPBT : 1;
-    a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;              // v8 grad_x operand
-    a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-    const int nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
+    int nwblk;
+    const ModulePrep a = module_prep_args(g, x, weight, alpha_act, alpha_weight, has_alpha ? alpha_cim : nullptr,
+                                          binary_mask, signed_act, c, &nwblk);
+    if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, a);
     prof_end(slot, s);
@@ -451,12 +473,8 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
                                 float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
                                 Pending* pend, void* stream) {
   Geo g;
-  CIMQ_TRY(make_geo(d, &g));
-  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
-  if (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN)
-    return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
   LsqArgs la;
-  CIMQ_TRY(lsq_args(g, q, &la));
+  CIMQ_TRY(module_geo(d, q, &g, &la));
   (void)alpha_act; (void)alpha_weight; (void)binary_mask;
   if (!grad_out || !x || !weight || !signed_act || !ctx || !grad_x || !grad_weight || !grad_alpha_act ||
       !grad_alpha_weight || !ws)
@@ -470,7 +488,7 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   uint8_t* w = reinterpret_cast<uint8_t*>(ws);
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
-  const float* scal = reinterpret_cast<const float*>(c + L.lsq_scal);
+  const float* scal = reinterpret_cast<const float*>(wreg(g, c) + L.lsq_scal);
   const float* sa = scal;
   const float* sw = scal + 1;
   const Plan3 p = v3_plan(g);
@@ -563,10 +581,8 @@ int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, c
                               const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
                               float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream) {
   Geo g;
-  CIMQ_TRY(make_geo(d, &g));
-  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
   LsqArgs la;
-  CIMQ_TRY(lsq_args(g, q, &la));
+  CIMQ_TRY(module_geo(d, q, &g, &la));
   if (!weight || !ctx || !grad_weight || !grad_alpha_act || !grad_alpha_weight || !ws)
     return fail(CIMQ_EINVAL, "null pointer argument");
   const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
@@ -576,6 +592,47 @@ int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, c
   return module_tail(g, la, q, reinterpret_cast<const uint8_t*>(ctx), reinterpret_cast<uint8_t*>(ws), weight,
                      alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim,
                      reinterpret_cast<hipStream_t>(stream));
+}
+
+int cimq_module_prepare(int n, const cimq_prepare_item* items, void* stream) {
+  if (n < 0 || (n > 0 && !items)) return fail(CIMQ_EINVAL, "bad prepare item list");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  PrepPack pk;
+  memset(&pk, 0, sizeof(pk));
+  int grid = 0;
+  for (int i = 0; i < n; ++i) {
+    const cimq_prepare_item& it = items[i];
+    Geo g;
+    LsqArgs la;
+    if (!it.lsq) return fail(CIMQ_EINVAL, "item %d: null LSQ descriptor", i);
+    cimq_lsq_desc q = *it.lsq;
+    q.flags = 0;
+    q.wprep = it.wprep;
+    CIMQ_TRY(module_geo(it.desc, &q, &g, &la));
+    if (!it.weight || !it.alpha_act || !it.alpha_weight || !it.binary_mask || !it.wprep)
+      return fail(CIMQ_EINVAL, "item %d: null pointer argument", i);
+    const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
+    if (has_alpha && (!it.alpha_cim || la.nbits_alpha == 0))
+      return fail(CIMQ_EINVAL, "item %d: adc 1 / 1.5 need alpha_cim", i);
+    if (!has_alpha) la.nbits_alpha = 0;
+    PrepJob& j = pk.job[pk.n];
+    j.g = g;
+    j.q = la;
+    j.a = module_prep_args(g, nullptr, it.weight, it.alpha_act, it.alpha_weight, has_alpha ? it.alpha_cim : nullptr,
+                           it.binary_mask, nullptr, nullptr, &j.nwblk);
+    j.a.nact_blocks = 0;
+    pk.blk0[pk.n] = grid;
+    grid += j.nwblk;
+    ++pk.n;
+    if (pk.n == kPrepJobs || i == n - 1) {
+      pk.blk0[pk.n] = grid;
+      hipLaunchKernelGGL(prep_weights_many_kernel, dim3(grid), dim3(256), 0, s, pk);
+      CIMQ_TRY(check_hip("prep_weights_many"));
+      memset(&pk, 0, sizeof(pk));
+      grid = 0;
+    }
+  }
+  return CIMQ_OK;
 }
 
 int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, const float* sa,

@@ -36,6 +36,7 @@ struct Geo {
   int variant;             // AdcVariant; anything but VAR_LIBRARY runs the literal (general) kernels
   int ps_int8;             // partial sums pass an int8 buffer before the ADC (scale_shift.py:401)
   uint32_t seed_lo, seed_hi;  // VAR_STOCHASTIC: Philox key
+  const unsigned char* wbase;  // host side: the weight-side ctx regions (cimq_lsq_desc.wprep); null: inside ctx
 };
 
 // Per-(tile i, a-slice j, w-slice k, out-channel o) ADC / STE parameters, SoA.

@@ -145,9 +145,14 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
   return CIMQ_OK;
 }
 
+// ctx: the weight-side regions first ([0, wbytes): weight operand fragments, ADC / STE
+// parameters, the module's step sizes -- functions of the parameters only, so a prepared
+// buffer (cimq_module_prepare, cimq_lsq_desc.wprep) can hold them instead), then the
+// activation-side regions (slice words, state words) of one forward.
 struct CtxLayout {
   size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
+  size_t wbytes;    // end of the weight-side regions
   size_t total;
 };
 
@@ -155,8 +160,6 @@ inline CtxLayout ctx_layout(const Geo& g) {
   CtxLayout L;
   size_t o = 0;
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
-  L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);  // forward slice bytes
-  L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
   L.wtc = o; o = align256(o + (size_t)g.T * g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
@@ -170,18 +173,27 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.beta = o; o = align256(o + npar * 4);
   L.ckj = o; o = align256(o + 3 * 64 * 4);
   L.flags = o; o = align256(o + 16);
+  L.lsq_scal = o; o = align256(o + 16 * 4);
+  L.wbytes = o;
+  L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);  // forward slice bytes
+  L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
   // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three
   // 64-bit planes for w8a8) per (tile, pixel, channel)
   L.st = o; o = align256(o + std::max((size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4), (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24)));
-  L.lsq_scal = o; o = align256(o + 16 * 4);
   L.total = o;
   return L;
 }
 
-inline Params params_of(const Geo& g, uint8_t* base) {
+// base of the weight-side regions of a ctx: the prepared buffer when the call has one
+inline uint8_t* wreg(const Geo& g, const uint8_t* ctx) {
+  return const_cast<uint8_t*>(g.wbase ? g.wbase : ctx);
+}
+
+inline Params params_of(const Geo& g, uint8_t* ctx) {
   CtxLayout L = ctx_layout(g);
+  uint8_t* base = wreg(g, ctx);
   Params p;
   p.thi = reinterpret_cast<int*>(base + L.thi);
   p.tlo = reinterpret_cast<int*>(base + L.tlo);

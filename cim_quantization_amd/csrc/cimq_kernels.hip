@@ -76,9 +76,13 @@ __device__ inline void act_item(const Geo& g, const float* __restrict__ x, float
 // case: fl(fl(r*sa)/sa) == r) the floor / remainder chain of slicing_act(_signed) reduces to
 // shifts and masks of that integer, bit for bit (floor-mod by 2^b of an integer is its low b
 // bits in two's complement); other values (the 6 - eps slice artifacts) take the float path.
-template <int NBP>
+// NBA_C > 0: nba = NBA_C and bsa = 1 at compile time (the unrolled digit loop has no runtime
+// bounds); 0: read from g
+template <int NBP, int NBA_C = 0>
 __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint32_t (&fwd)[NBP / 4],
                                  uint32_t (&bwd)[NBP / 4]) {
+  const int nba = NBA_C > 0 ? NBA_C : g.nba;
+  const int bsa = NBA_C > 0 ? 1 : g.bsa;
   float xq;
   if (g.input_kind == 1) {
     const float t = v / sa;
@@ -91,7 +95,7 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
   }
   const float xi = xq / sa;
   const int xhi = to_i8_wrap(xi);
-  const int mask = (1 << g.bsa) - 1;
+  const int mask = (1 << bsa) - 1;
   // forward digits without branches for |xi| < 2^23: with F = floor(m) and fr = m - F (both
   // exact), m = xi (unsigned) or |xi| (signed, digits negated for xi < 0), the reference's
   // chain gives digit 0 = rint((F mod 2^b) + fr) -- 2^b for the 6 - eps artifacts -- and digit
@@ -107,8 +111,8 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
   for (int w = 0; w < NBP / 4; ++w) { fwd[w] = 0u; bwd[w] = 0u; }
 #pragma unroll
   for (int j = 0; j < NBP; ++j) {
-    if (j < g.nba) {
-      const int sh = g.bsa * j;
+    if (j < nba) {
+      const int sh = bsa * j;
       const int sb = sgn ? (xhi >= 0 ? ((xhi >> sh) & mask) : -(((-xhi) >> sh) & mask)) : ((xhi >> sh) & mask);
       int d = (j == 0) ? min((int)rintf((float)(Fi & mask) + fr), 127) : ((Fi >> sh) & mask);
       const int sf = negd ? -d : d;
@@ -121,8 +125,8 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
     for (int w = 0; w < NBP / 4; ++w) fwd[w] = 0u;
 #pragma unroll
     for (int j = 0; j < NBP; ++j) {
-      if (j < g.nba) {
-        const int sf = clamp_i8(sgn ? slice_signed(xi, j, g.bsa) : slice_unsigned(xi, j, g.bsa));
+      if (j < nba) {
+        const int sf = clamp_i8(sgn ? slice_signed(xi, j, bsa) : slice_unsigned(xi, j, bsa));
         fwd[j >> 2] |= (uint32_t)(uint8_t)(int8_t)sf << (8 * (j & 3));
       }
     }
@@ -130,7 +134,7 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
 }
 
 // four consecutive elements (idx4 = 4 * t): one 16-B load, 16-B (NBP 4) or 2 x 16-B stores
-template <int NBP>
+template <int NBP, int NBA_C = 0>
 __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
                                  uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long t) {
   const float4 v4 = reinterpret_cast<const float4*>(x)[t];
@@ -143,7 +147,7 @@ __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, floa
     for (int w = 0; w < NBP / 4; ++w) f[e][w] = b[e][w] = __float_as_uint(vv[e]);
 #else
 #pragma unroll
-  for (int e = 0; e < 4; ++e) act_words<NBP>(g, vv[e], sa, sgn, f[e], b[e]);
+  for (int e = 0; e < 4; ++e) act_words<NBP, NBA_C>(g, vv[e], sa, sgn, f[e], b[e]);
 #endif
   if (NBP == 4) {
     reinterpret_cast<uint4*>(xcf)[t] = make_uint4(f[0][0], f[1][0], f[2][0], f[3][0]);
@@ -162,7 +166,17 @@ __device__ inline void act_range(const Geo& g, const float* __restrict__ x, floa
                                  long long step) {
   if (g.Nin % 4 == 0) {
     const long long n4 = g.Nin / 4;
-    if (g.NBP == 4)
+    // the 1-bit-slice cases of the CIFAR / QuantLinear configs with compile-time digit loops
+    const int sel = g.bsa != 1 ? 0 : g.nba;
+    if (sel == 3)
+      for (long long t = first; t < n4; t += step) act_item4<4, 3>(g, x, sa, sgn, xcf, xcb, t);
+    else if (sel == 2)
+      for (long long t = first; t < n4; t += step) act_item4<4, 2>(g, x, sa, sgn, xcf, xcb, t);
+    else if (sel == 4)
+      for (long long t = first; t < n4; t += step) act_item4<4, 4>(g, x, sa, sgn, xcf, xcb, t);
+    else if (sel == 8)
+      for (long long t = first; t < n4; t += step) act_item4<8, 8>(g, x, sa, sgn, xcf, xcb, t);
+    else if (g.NBP == 4)
       for (long long t = first; t < n4; t += step) act_item4<4>(g, x, sa, sgn, xcf, xcb, t);
     else
       for (long long t = first; t < n4; t += step) act_item4<8>(g, x, sa, sgn, xcf, xcb, t);

@@ -39,35 +39,42 @@ struct ModulePrep {
   int nwf, nwg, nwt, nwc, npp;  // items of the weight-side roles
 };
 
-__global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, ModulePrep a) {
-  __shared__ float4 red4[16];
-  float* red = reinterpret_cast<float*>(red4);
+// the weight side of the prologue: block wb of nwblk (quantised weight operands, alpha_cim's
+// quantiser into the ADC thresholds, and in block 0 the step sizes / literal-ADC flag)
+__device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const ModulePrep& a, int wb, int nwblk,
+                                           float* red) {
   const float sa = grad_scale_value(a.alpha_act[0], q.gs_a);  // lsq.py:547-548
-  // the few weight-side blocks go first so their latency-bound work overlaps the act stream
-  const int nwblk = (int)gridDim.x - a.nact_blocks;
-  if ((int)blockIdx.x >= nwblk) {
-#ifdef CIMQ_EXP_PREP_NOACT
-    return;
-#endif
-    const int ab = (int)blockIdx.x - nwblk;
-    const bool sgn = a.signed_act[0] != 0.f;
-    act_range(g, a.x, sa, sgn, a.xcf, a.xcb, (long long)ab * blockDim.x + threadIdx.x,
-              (long long)a.nact_blocks * blockDim.x);
-    return;
-  }
-#ifdef CIMQ_EXP_PREP_NOWT
-  return;
-#endif
   const float sw = grad_scale_value(a.alpha_w[0], q.gs_w);  // lsq.py:553-554
   ASrc as{nullptr, 1, 0.f, 0.f};
   float mx = 0.f, mn = 0.f;
+  // alpha_cim is read once into registers when it fits (<= AP per thread): every load in
+  // flight together, not one dependent round trip per loop iteration
+  constexpr int AP = 16;
+  float av[AP];
+  const bool inreg = q.nalpha <= AP * (int)blockDim.x;
   if (q.nbits_alpha > 0) {  // lsq.py:566-571
     mx = -INFINITY;
     mn = INFINITY;
-    for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
-      const float v = a.alpha_cim[e];
-      mx = (v != v || mx != mx) ? v + mx : fmaxf(mx, v);
-      mn = (v != v || mn != mn) ? v + mn : fminf(mn, v);
+    if (inreg) {
+#pragma unroll
+      for (int u = 0; u < AP; ++u) {
+        const int e = threadIdx.x + u * (int)blockDim.x;
+        av[u] = e < q.nalpha ? a.alpha_cim[e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < AP; ++u) {
+        if ((int)threadIdx.x + u * (int)blockDim.x < q.nalpha) {
+          const float v = av[u];
+          mx = (v != v || mx != mx) ? v + mx : fmaxf(mx, v);
+          mn = (v != v || mn != mn) ? v + mn : fminf(mn, v);
+        }
+      }
+    } else {
+      for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
+        const float v = a.alpha_cim[e];
+        mx = (v != v || mx != mx) ? v + mx : fmaxf(mx, v);
+        mn = (v != v || mn != mn) ? v + mn : fminf(mn, v);
+      }
     }
     const float2 r = block_max_min(mx, mn, red);
     mx = r.x;
@@ -77,17 +84,25 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
     as.qp_al = (float)((1 << q.nbits_alpha) - 1);
   }
   const WSrc ws{a.weight, sw, 1, q.qn_w, q.qp_w};  // lsq.py:555
-  const int wb = (int)blockIdx.x;
   if (wb == 0) {
     // literal-ADC flag: any entry whose alpha_q / scales break the threshold search
     bool lit = false;
     if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
       lit = !scales_ok(sw, sa);
-      if (as.a)
+      if (as.a && inreg) {
+#pragma unroll
+        for (int u = 0; u < AP; ++u) {
+          if ((int)threadIdx.x + u * (int)blockDim.x < q.nalpha) {  // as ASrc::get on the loaded value
+            const float v = clamp_nan(round_pass_value(av[u] / as.scale), 1.f, as.qp_al) * as.scale;
+            lit = lit || !(v > 0.f && isfinite(v));
+          }
+        }
+      } else if (as.a) {
         for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) {
           const float v = as.get(e);
           lit = lit || !(v > 0.f && isfinite(v));
         }
+      }
     }
     lit = __syncthreads_or(lit);
     if (threadIdx.x == 0) {
@@ -114,6 +129,54 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
     else if (t < e4) wcy_item(g, ws, a.ncpbt, a.wcy, t - e3);
     else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4);
   }
+}
+
+__global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, ModulePrep a) {
+  __shared__ float4 red4[16];
+  float* red = reinterpret_cast<float*>(red4);
+  // the few weight-side blocks go first so their latency-bound work overlaps the act stream
+  // (none when the weight side was prepared beforehand: cimq_module_prepare)
+  const int nwblk = (int)gridDim.x - a.nact_blocks;
+  if ((int)blockIdx.x >= nwblk) {
+#ifdef CIMQ_EXP_PREP_NOACT
+    return;
+#endif
+    const float sa = grad_scale_value(a.alpha_act[0], q.gs_a);  // lsq.py:547-548
+    const int ab = (int)blockIdx.x - nwblk;
+    const bool sgn = a.signed_act[0] != 0.f;
+    act_range(g, a.x, sa, sgn, a.xcf, a.xcb, (long long)ab * blockDim.x + threadIdx.x,
+              (long long)a.nact_blocks * blockDim.x);
+    return;
+  }
+#ifdef CIMQ_EXP_PREP_NOWT
+  return;
+#endif
+  module_prep_weights(g, q, a, (int)blockIdx.x, nwblk, red);
+}
+
+// The weight side of several layers' prologues in one launch (cimq_module_prepare): a layer's
+// weight work is a few latency-bound blocks, so packing the layers of a network into one grid
+// pays that latency once instead of once per layer.  The jobs travel as kernel arguments.
+struct PrepJob {
+  Geo g;
+  LsqArgs q;
+  ModulePrep a;
+  int nwblk;
+};
+constexpr int kPrepJobs = 7;
+struct PrepPack {
+  int n;
+  int blk0[kPrepJobs + 1];  // first block of each job, blk0[n] = grid
+  PrepJob job[kPrepJobs];
+};
+static_assert(sizeof(PrepPack) <= 4000, "PrepPack exceeds the kernel-argument budget");
+
+__global__ __launch_bounds__(256) void prep_weights_many_kernel(PrepPack p) {
+  __shared__ float4 red4[16];
+  int j = 0;
+  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  module_prep_weights(p.job[j].g, p.job[j].q, p.job[j].a, (int)blockIdx.x - p.blk0[j], p.job[j].nwblk,
+                      reinterpret_cast<float*>(red4));
 }
 
 __global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q, ModuleTail a) {

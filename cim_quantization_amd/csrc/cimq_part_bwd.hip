@@ -31,7 +31,7 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
       auto kern = g.KS == 1 ? cim_bwd_gw_v3_kernel<NBP, 1, FBMAX, true> : cim_bwd_gw_v3_kernel<NBP, 2, FBMAX, true>;
       CIMQ_TRY(set_lds(kern, lds));
       hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
-                         reinterpret_cast<const v4i*>(ctx + L.wfrag), pp, sw, sa, gout, W.rows,
+                         reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag), pp, sw, sa, gout, W.rows,
                          reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
       return check_hip("cim_bwd_gw_v3(init)");
     }
@@ -41,7 +41,7 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;
     CIMQ_TRY(set_lds(kern, lds));
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
-                       reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(ctx + L.wfrag),
+                       reinterpret_cast<const int8_t*>(ctx + L.xhat), reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag),
                        pp, sw, sa, signed_act, gout, W.rows, reinterpret_cast<float*>(ws + W.gw_slab),
                        reinterpret_cast<float*>(ws + W.ga_slab), reinterpret_cast<float*>(ws + W.gb_slab));
   }
@@ -56,8 +56,8 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   const Plan3 p = v3_plan(g);
-  const v4i* wf = reinterpret_cast<const v4i*>(ctx + L.wfrag);
-  const v4i* wg = reinterpret_cast<const v4i*>(ctx + L.wgx);
+  const v4i* wf = reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag);
+  const v4i* wg = reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wgx);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   *lsq_fused = false;
   if (p.ok) {
@@ -71,7 +71,7 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
       CIMQ_TRY(set_lds(kern, p.lds_gx6));
       const int slot = prof_begin(KID_BWD_GX, g, s);
       hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx6, s, g, p.v, ctx + L.st,
-                         reinterpret_cast<const uint4*>(ctx + L.wtc), pp, sw, sa, gout, x, gx, part);
+                         reinterpret_cast<const uint4*>(wreg(g, ctx) + L.wtc), pp, sw, sa, gout, x, gx, part);
       prof_end(slot, s);
       *lsq_fused = lsq;
       return check_hip("cim_bwd_gx_v6");
@@ -81,7 +81,7 @@ int launch_gx(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_BWD_GX, g, s);
     hipLaunchKernelGGL(kern, grid, dim3(512), p.lds_gx, s, g, p.v, ctx + L.st,
-                       reinterpret_cast<const uint4*>(ctx + L.wtc), pp, sw, sa, gout, x, gx, part);
+                       reinterpret_cast<const uint4*>(wreg(g, ctx) + L.wtc), pp, sw, sa, gout, x, gx, part);
     prof_end(slot, s);
     *lsq_fused = lsq;
     return check_hip("cim_bwd_gx_v5");

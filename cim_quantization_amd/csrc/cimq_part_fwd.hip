@@ -32,7 +32,7 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
   dim3 grid(std::min(p.v.nmt, tune("FWD_GRID", NBP == 8 ? 1024 : 768)), cdiv(g.OB16, obm));
   const int slot = prof_begin(cst ? KID_FWD_V7 : KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), p.lds_fwd, s, g, p.v, ctx + L.xcode,
-                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);
+                     reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag), params_of(g, ctx), sw, sa, out, ctx + L.st);
   prof_end(slot, s);
   return check_hip("cim_fwd_v3");
 }
@@ -58,7 +58,7 @@ int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, flo
   CIMQ_TRY(set_lds(kern, lds));
   const int slot = DBG ? -1 : prof_begin(KID_FWD, g, s);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, g, reinterpret_cast<const int8_t*>(ctx + L.xcode),
-                     reinterpret_cast<const v4i*>(ctx + L.wfrag), params_of(g, ctx), sw, sa, out, ps_dbg,
+                     reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag), params_of(g, ctx), sw, sa, out, ps_dbg,
                      adc_dbg);
   prof_end(slot, s);
   return check_hip("cim_fwd");

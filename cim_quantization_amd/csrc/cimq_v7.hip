@@ -251,6 +251,10 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
           if (cb + NPART < ncb) {
 #pragma unroll
             for (int s = 0; s < NKS; ++s) anx[s] = wt[((cb + NPART) * NKS + s) * 64];
+#ifdef CIMQ_EXP_GX_NOWLOAD
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) anx[s] = v4i{lane, s, cb, i};
+#endif
           }
           v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll

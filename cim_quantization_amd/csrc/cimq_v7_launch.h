@@ -28,7 +28,7 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_GX_V8, g, s);
     hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands + (carry.finish ? 1 : 0)), dim3(256 * np), p.lds_gx, s, g, p.v, st,
-                       reinterpret_cast<const v4i*>(ctx + L.wcy), pp, sw, sa, gout, x, gx,
+                       reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wcy), pp, sw, sa, gout, x, gx,
                        reinterpret_cast<float*>(ws + W.lsq_part), carry);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("cim_bwd_gx_v8"));

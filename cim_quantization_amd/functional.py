@@ -17,6 +17,7 @@ Device-only: CPU tensors raise (there is no CPU fallback in the product path).
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import math
 
 import torch
@@ -390,6 +391,89 @@ def chained_epilogues(device=None):
             ch.flush()
 
 
+class WeightPrep:
+    """The weight side of one Conv2dLSQCiM forward, computed ahead by ``prepare_weights``
+    (cimq_module_prepare): the buffer, the descriptors it was made for and the parameter
+    versions it saw.  A forward takes it once (``take``) if all three still match."""
+
+    __slots__ = ("buf", "key", "versions")
+
+    def __init__(self, buf, key, versions):
+        self.buf, self.key, self.versions = buf, key, versions
+
+
+def _prep_key(desc, lsq, x_shape):
+    return (bytes(desc), lsq.qn_w, lsq.qp_w, lsq.gscale_a, lsq.gscale_w, lsq.nbits_alpha, tuple(x_shape))
+
+
+def _versions(*ts):
+    return tuple(-1 if t is None else t._version for t in ts)
+
+
+def _module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits,
+                  xbar, nbits_alpha, has_alpha, stochastic):
+    B, C, H, W = x_shape
+    O, _, KH, KW = weight.shape
+    st = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
+    pd = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
+    qp_a = float(2 ** nbits_a - 1)
+    qn_w, qp_w = -(2 ** (nbits_w - 1)), 2 ** (nbits_w - 1) - 1
+    desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
+                          abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a,
+                          _lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
+                          stochastic_seed() if stochastic else 0)
+    lsq = _lib.make_lsq_desc(qn_w, qp_w, 1.0 / math.sqrt(B * C * H * W * qp_a),
+                             1.0 / math.sqrt(weight.numel() * qp_w), nbits_alpha if has_alpha else 0)
+    return desc, lsq
+
+
+def prepare_weights(modules, stream=None):
+    """Run the weight side of the next forward of every fused Conv2dLSQCiM in ``modules`` (the
+    weight and alpha_cim quantisers into the CiM operands and ADC thresholds, lsq.py:552-571) in
+    one library call, ahead of the forwards: each layer's forward then only quantises its
+    activation.  Call it after the parameters are final for the step (after the optimizer step,
+    before the forward pass); a forward whose parameters or input shape changed since, or that
+    finds no prepared state, does the whole prologue itself, as without this call.  Layers still
+    in their first (initialising) step, stochastic-ADC layers and non-fused paths are skipped."""
+    items, keep, taken = [], [], []
+    dev = None
+    for m in modules:
+        if not getattr(m, "_fused_ready", None) or not m._fused_ready():
+            continue
+        shape = m._last_x_shape
+        has_alpha = m.alpha_cim is not None
+        desc, lsq = _module_descs(shape, m.weight, m.stride, m.padding, m.dilation, m.nbits_a, m.abitslice,
+                                  m.nbits_w, m.wbitslice, m.adcbits, m.xbar, m.nbits_alpha, has_alpha, False)
+        sizes = _lib.query_sizes(desc)
+        dev = m.weight.device
+        buf = torch.empty(max(sizes.wprep_bytes, 1), device=dev, dtype=torch.uint8)
+        bm = m.binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+        ps = (m.weight, m.alpha_act, m.alpha_weight, m.alpha_cim)
+        for t in ps:
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+                raise ValueError("prepare_weights: parameters must be contiguous fp32")
+        it = _lib.PrepareItem()
+        it.desc = ctypes.pointer(desc)
+        it.lsq = ctypes.pointer(lsq)
+        it.weight = m.weight.data_ptr()
+        it.alpha_act = m.alpha_act.data_ptr()
+        it.alpha_weight = m.alpha_weight.data_ptr()
+        it.alpha_cim = m.alpha_cim.data_ptr() if has_alpha else None
+        it.binary_mask = bm.data_ptr()
+        it.wprep = buf.data_ptr()
+        items.append(it)
+        keep.append((desc, lsq, bm))
+        taken.append((m, WeightPrep(buf, _prep_key(desc, lsq, shape), _versions(*ps, m.binary_mask))))
+    if not items:
+        return 0
+    arr = (_lib.PrepareItem * len(items))(*items)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.load().cimq_module_prepare(len(items), arr, s), "cimq_module_prepare")
+    for m, wp in taken:
+        m._wprep = wp
+    return len(items)
+
+
 class _CimModuleConv(torch.autograd.Function):
     """A whole Conv2dLSQCiM layer after its first-step init (lsq.py:544-581): the activation,
     weight and alpha_cim quantisers run inside libcimq on the raw parameters (no torch ops,
@@ -408,19 +492,18 @@ class _CimModuleConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                 dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False,
-                stochastic=False, tail_stream=None):
+                stochastic=False, tail_stream=None, wprep=None):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
-        qp_a = float(2 ** nbits_a - 1)
-        qn_w, qp_w = -(2 ** (nbits_w - 1)), 2 ** (nbits_w - 1) - 1
-        desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
-                              abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a,
-                              _lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
-                              stochastic_seed() if stochastic else 0)
-        lsq = _lib.make_lsq_desc(qn_w, qp_w, 1.0 / math.sqrt(x.numel() * qp_a),
-                                 1.0 / math.sqrt(weight.numel() * qp_w),
-                                 nbits_alpha if alpha_cim is not None else 0)
+        desc, lsq = _module_descs(tuple(x.shape), weight, st, pd, dilation, nbits_a, abitslice, nbits_w, wbitslice,
+                                  adcbits, xbar, nbits_alpha, alpha_cim is not None, stochastic)
+        # a prepared weight side (prepare_weights) if it was made for exactly this call
+        ctx.wprep_buf = None
+        if (wprep is not None and not stochastic and wprep.key == _prep_key(desc, lsq, x.shape)
+                and wprep.versions == _versions(weight, alpha_act, alpha_weight, alpha_cim, binary_mask)):
+            lsq.wprep = wprep.buf.data_ptr()
+            ctx.wprep_buf = wprep.buf
         sizes = _lib.query_sizes(desc)
         xc = x.detach().to(torch.float32).contiguous()
         wc = weight.detach().to(torch.float32).contiguous()
@@ -478,7 +561,8 @@ class _CimModuleConv(torch.autograd.Function):
         if targets is not None:
             gw, gaa, gaw, gac = targets
             lsq = _lib.make_lsq_desc(lsq.qn_w, lsq.qp_w, lsq.gscale_a, lsq.gscale_w, lsq.nbits_alpha,
-                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS | (_lib.CIMQ_LSQ_SKIP_TAIL if side else 0))
+                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS | (_lib.CIMQ_LSQ_SKIP_TAIL if side else 0),
+                                     lsq.wprep)
         else:
             gw = torch.empty_like(wc)
             gaa = torch.empty(1, device=dev, dtype=torch.float32)
@@ -504,8 +588,8 @@ class _CimModuleConv(torch.autograd.Function):
                                                       gaa.data_ptr(), gaw.data_ptr(),
                                                       None if gac is None else gac.data_ptr(), ws.data_ptr(),
                                                       ch.pending, stream), "cimq_module_backward_chain")
-            ch.keep = (ws, cbuf, wc, ac, gw, gaa, gaw, gac)
-            return (gx,) + (None,) * 19
+            ch.keep = (ws, cbuf, wc, ac, gw, gaa, gaw, gac, ctx.wprep_buf)
+            return (gx,) + (None,) * 20
         _lib.check(lib.cimq_module_backward(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
                                             aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),
                                             bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(),
@@ -522,22 +606,24 @@ class _CimModuleConv(torch.autograd.Function):
                                                          gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
                                                          None if gac is None else gac.data_ptr(), ws.data_ptr(),
                                                          side.cuda_stream), "cimq_module_backward_tail")
-            for t in (ws, cbuf, wc) + ((ac,) if ac is not None else ()):
+            for t in (ws, cbuf, wc) + ((ac,) if ac is not None else ()) + \
+                    ((ctx.wprep_buf,) if ctx.wprep_buf is not None else ()):
                 t.record_stream(side)
         if targets is not None:
-            return (gx,) + (None,) * 19
-        return (gx, gw, gaa, gaw, gac) + (None,) * 15
+            return (gx,) + (None,) * 20
+        return (gx, gw, gaa, gaw, gac) + (None,) * 16
 
 
 def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                     dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha,
-                    accumulate=False, stochastic=False, tail_stream=None):
+                    accumulate=False, stochastic=False, tail_stream=None, wprep=None):
     """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
     the three step-size parameters (alpha_act and alpha_weight are 1-element tensors).
-    ``accumulate`` / ``tail_stream``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC."""
+    ``accumulate`` / ``tail_stream``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC;
+    ``wprep``: a WeightPrep from prepare_weights (used only if it matches this call)."""
     return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
                                 padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
-                                nbits_alpha, accumulate, stochastic, tail_stream)
+                                nbits_alpha, accumulate, stochastic, tail_stream, wprep)
 
 
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,

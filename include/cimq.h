@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 6
+#define CIMQ_ABI_VERSION 7
 
 /* status codes */
 #define CIMQ_OK 0
@@ -97,13 +97,18 @@ typedef struct cimq_lsq_desc {
   float gscale_w;           /* grad_scale factor of alpha_weight: 1/sqrt(numel(w) * Qp_w) (lsq.py:553) */
   int32_t nbits_alpha;      /* alpha_cim quantiser bits (lsq.py:566-571); ignored unless adc 1 / 1.5 */
   int32_t flags;            /* CIMQ_LSQ_* bits */
-  int32_t reserved[2];
+  const void* wprep;        /* NULL, or a buffer of cimq_sizes.wprep_bytes that cimq_module_prepare
+                               filled for this descriptor pair and the current parameter values:
+                               the module forward then runs only the activation quantiser, and it
+                               and the backward read the weight-side state (w_q operands, alpha_q
+                               thresholds, step sizes) from there instead of from ctx */
 } cimq_lsq_desc;
 
 typedef struct cimq_sizes {
   size_t ctx_bytes;           /* forward -> backward state, caller-owned device memory */
   size_t fwd_workspace_bytes; /* scratch for cimq_forward / cimq_alpha_init */
   size_t bwd_workspace_bytes; /* scratch for cimq_backward */
+  size_t wprep_bytes;         /* weight-side state of the module entry points (cimq_module_prepare) */
 } cimq_sizes;
 
 /* ABI version of the loaded library (compare with CIMQ_ABI_VERSION). */
@@ -169,6 +174,28 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
 int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
                               const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
                               float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
+
+/* One layer of cimq_module_prepare: its descriptors (as the forward will receive them; the
+ * lsq descriptor's wprep and flags are ignored here) and raw parameters, and its output buffer
+ * ``wprep`` (cimq_sizes.wprep_bytes, caller-owned device memory). */
+typedef struct cimq_prepare_item {
+  const cimq_conv_desc* desc;
+  const cimq_lsq_desc* lsq;
+  const float* weight;
+  const float* alpha_act;
+  const float* alpha_weight;
+  const float* alpha_cim; /* NULL unless adc_bits is 1 or 1.5 */
+  const int8_t* binary_mask;
+  void* wprep;
+} cimq_prepare_item;
+
+/* The weight side of cimq_module_forward for n layers at once (lsq.py:552-571: w_q, alpha_q and
+ * the step sizes, turned into the CiM kernels' operands and ADC / STE thresholds): one launch per
+ * up to 7 layers instead of a few latency-bound workgroups inside every layer's prologue.  A
+ * forward given q->wprep = items[i].wprep must see the same parameter values (e.g. prepare after
+ * each optimizer step); the backward of that forward reads the buffer too, so it must not be
+ * re-prepared in between. */
+int cimq_module_prepare(int n, const cimq_prepare_item* items, void* stream);
 
 /* Opaque, caller-owned host memory for cimq_module_backward_chain: zero-initialise it once. */
 typedef struct cimq_pending {

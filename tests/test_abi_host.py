@@ -96,3 +96,39 @@ def test_ctypes_arity_matches_header(lib):
     assert set(ar) == set(L.EXPORTED_SYMBOLS)
     for sym, n in ar.items():
         assert len(getattr(lib, sym).argtypes) == n, sym
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors have the header's sizes and field offsets (gcc on include/cimq.h)."""
+    import subprocess
+    mirrors = {"cimq_conv_desc": L.ConvDesc, "cimq_lsq_desc": L.LsqDesc, "cimq_sizes": L.Sizes,
+               "cimq_prepare_item": L.PrepareItem, "cimq_qconv_desc": L.QConvDesc}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "cimq.h"', 'int main(void) {']
+    for cname, cls in mirrors.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'  printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ['  return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, got):
+        cname, fname, v = line.split()
+        cls = mirrors[cname]
+        want = ctypes.sizeof(cls) if fname == "size" else getattr(cls, fname).offset
+        assert int(v) == want, line
+
+
+def test_module_prepare_validates_items(lib):
+    d = _desc(input_kind=L.CIMQ_INPUT_RAW_LSQ, lsq_qp=7.0)
+    q = L.make_lsq_desc(-4, 3, 1e-3, 1e-3, 8)
+    it = L.PrepareItem()
+    it.desc, it.lsq = ctypes.pointer(d), ctypes.pointer(q)
+    arr = (L.PrepareItem * 1)(it)
+    assert lib.cimq_module_prepare(1, arr, None) == 1  # null parameter pointers
+    assert "null" in lib.cimq_last_error().decode()
+    assert lib.cimq_module_prepare(-1, None, None) == 1
+    assert lib.cimq_module_prepare(0, None, None) == 0
+    assert L.query_sizes(d).wprep_bytes > 0

@@ -28,6 +28,7 @@ VARIANTS = {
     "gw_noga_nomfma_nod": ["CIMQ_EXP_GW_NOGA", "CIMQ_EXP_GW_NOMFMA", "CIMQ_EXP_GW_NOD"],
     "gx_nomfma": ["CIMQ_EXP_GX_NOMFMA"],
     "gx_noring": ["CIMQ_EXP_GX_NORING"],
+    "gx_nowload": ["CIMQ_EXP_GX_NOWLOAD"],
     "fwd_nost": ["CIMQ_EXP_FWD_NOST"],
     "gx_nofold": ["CIMQ_EXP_GX_NOFOLD"],
     "gx_nostate": ["CIMQ_EXP_GX_NOSTATE"],
