@@ -296,5 +296,6 @@ __device__ inline void split3(float a, uint16_t& hi, uint16_t& mid, uint16_t& lo
 }
 
 __device__ inline v8bf as_v8bf(v4i x) { return __builtin_bit_cast(v8bf, x); }
+__device__ inline v4i as_v4i(v8bf x) { return __builtin_bit_cast(v4i, x); }
 
 }  // namespace cimq

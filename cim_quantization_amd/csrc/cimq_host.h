@@ -376,7 +376,14 @@ inline Plan7 v7_plan(const Geo& g) {
   v.NPART = tune("GX_NPART", g.Wo >= 32 ? 1 : 2);
   if (v.NPART != 1 && v.NPART != 2 && v.NPART != 4) return p;
   if (g.NBP == 8 && v.NPART == 4) v.NPART = 2;  // 128-VGPR cap of 1024-thread blocks spills w8a8
-  p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (g.SH * v.SWD + 2) * 4) + 64 * 4 + 64;
+  // ring, mask coefficients (64 floats), per-wave partials (64 floats), and with NPART > 1 the G
+  // exchange [4 pixel groups][NKS][3][64 lanes][16 B] when it fits (GSH)
+  p.lds_gx = a16((size_t)v.RSLOT * v.NSEG * g.C * 3 * (g.SH * v.SWD + 2) * 4) + 64 * 4 + 64 * 4;
+  {
+    const size_t gsh = (size_t)4 * g.NKS * 3 * 64 * 16;
+    v.GSH = (v.NPART > 1 && g.OB16 <= 2 && tune("GX_GSH", 1) && p.lds_gx + gsh <= kLdsMax - 512) ? 1 : 0;
+    if (v.GSH) p.lds_gx += gsh;
+  }
   // grad_w
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
   v.CPITCH = v.NSLOT * g.Wo + 8;

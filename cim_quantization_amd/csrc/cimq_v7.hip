@@ -55,6 +55,8 @@ struct V7 {
   int whole;    // 1: a stage is 128/P whole images; 0: a stage is 128/Wo rows of one image
   int CPL;      // channels per staged plane: min(16, C)
   int NTL;      // most crossbar tiles touching one 16-channel block (grad_alpha LDS regions)
+  int GSH;      // grad_x, NPART > 1, at most 2 o-blocks: the NPART waves of a pixel group build disjoint G chunks and
+                // exchange them through LDS (else every wave builds all of them)
 };
 
 // pass-bit masks of the state word: all j of slice k / all k of slice j
@@ -132,6 +134,8 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
   float* ring = reinterpret_cast<float*>(smem);
   float* cel = ring + (size_t)v.RSLOT * rrow;
   float* red = cel + 64;
+  // G exchange (GSH): [pixel group][chunk s][hi, mid, lo][64 lanes] 16-byte operands
+  v4i* gsh = reinterpret_cast<v4i*>(red + 64);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -198,8 +202,11 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
         }
       }
       v8bf Gh[NKS], Gm[NKS], Gl[NKS];
+      // (not for 4 o-blocks: its 6 chunks already fill the register budget, the exchange spills)
+      const bool share = NPART > 1 && OBX <= 2 && v.GSH;
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
+        if (share && s % NPART != part) continue;  // built by another wave of this pixel group
         float Gv[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -229,6 +236,27 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
           }
         }
         split3x8(Gv, Gh[s], Gm[s], Gl[s]);
+      }
+      if (share) {
+        // every wave of the pixel group (same lanes, same pixels) publishes its chunks and
+        // takes the others'; the second barrier keeps the next tile's writes behind the reads
+        v4i* gq = gsh + (size_t)(wave & 3) * NKS * 3 * 64 + lane;
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+          if (s % NPART != part) continue;
+          gq[(s * 3 + 0) * 64] = as_v4i(Gh[s]);
+          gq[(s * 3 + 1) * 64] = as_v4i(Gm[s]);
+          gq[(s * 3 + 2) * 64] = as_v4i(Gl[s]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+          if (s % NPART == part) continue;
+          Gh[s] = as_v8bf(gq[(s * 3 + 0) * 64]);
+          Gm[s] = as_v8bf(gq[(s * 3 + 1) * 64]);
+          Gl[s] = as_v8bf(gq[(s * 3 + 2) * 64]);
+        }
+        __syncthreads();
       }
       const int cp_lo = (i * g.xbar) / 3, cp_hi = (min(g.K, (i + 1) * g.xbar) - 1) / 3;
       const int cpb_lo = cp_lo >> 2, ncb = (cp_hi >> 2) - cpb_lo + 1;
