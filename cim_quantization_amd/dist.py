@@ -138,3 +138,53 @@ class GradBucket:
         for m in modules:
             if hasattr(m, "_state_cache"):
                 m._state_cache = None  # init flags may have changed with the buffers
+
+
+class FlatSGD:
+    """``torch.optim.SGD`` (momentum, per-parameter weight decay, no dampening / Nesterov) over
+    the parameters of a GradBucket, on flat buffers.
+
+    The parameters move into one flat fp32 tensor laid out like the bucket's gradients (each
+    ``p.data`` becomes a view of it), so one step is four elementwise launches over every
+    parameter instead of torch's per-tensor-list foreach kernels (seven launches, 57 us per
+    ResNet-20 step).  Per element it is torch's SGD step:
+
+        d = g + wd * p;   buf = d (first step) or momentum * buf + d;   p = p - lr * buf
+
+    (the reference's optimizer, examples/__init__.py:184-188, with alpha_* out of weight decay).
+    Each step bumps the parameters' autograd version counters, as torch's in-place update of
+    the parameters would (functional.prepare_weights relies on them)."""
+
+    def __init__(self, bucket, lr, momentum=0.9, weight_decay=None):
+        """``weight_decay``: one float per parameter of ``bucket.params`` (0 for no decay)."""
+        self.bucket, self.lr, self.momentum = bucket, float(lr), float(momentum)
+        params = bucket.params
+        wds = [0.0] * len(params) if weight_decay is None else [float(w) for w in weight_decay]
+        if len(wds) != len(params):
+            raise ValueError("one weight decay per parameter")
+        self.flat = torch.empty_like(bucket.flat)
+        self.wd = torch.empty_like(bucket.flat)
+        off = 0
+        with torch.no_grad():
+            for p, w in zip(params, wds):
+                k = p.numel()
+                if p.dtype != torch.float32 or p.device != self.flat.device:
+                    raise ValueError("FlatSGD takes fp32 parameters on the bucket's device")
+                self.flat[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + k].view_as(p)
+                self.wd[off:off + k].fill_(w)
+                off += k
+        self.params = params
+        self.buf = torch.zeros_like(self.flat)
+        self.started = False
+
+    @torch.no_grad()
+    def step(self):
+        d = torch.addcmul(self.bucket.flat, self.wd, self.flat)  # g + wd * p
+        if self.started:
+            self.buf.mul_(self.momentum).add_(d)
+        else:
+            self.buf.copy_(d)
+            self.started = True
+        self.flat.add_(self.buf, alpha=-self.lr)
+        torch.autograd.graph.increment_version(self.params)
