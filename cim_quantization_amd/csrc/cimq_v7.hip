@@ -466,6 +466,12 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   float* cdl = reinterpret_cast<float*>(cur); cur += 64 * 4;
   float* red = reinterpret_cast<float*>(cur);  // [4 waves][NTL][NKJ][16] grad_alpha partials
   for (int t = threadIdx.x; t < NKJ; t += blockDim.x) cdl[t] = pp.ckj[2 * NKJ + t];
+  // the 8-element pad after the staged rows of each slice j's first plane (kw 0, channel 0) stays
+  // zero: A fragments of rows past C or of kernel rows outside the image read it, so one address
+  // select per row group replaces a select per fragment register
+  const int zoff = v.CPITCH - 8;
+  if (threadIdx.x < NBA)
+    *reinterpret_cast<uint4*>(pl + (size_t)threadIdx.x * 3 * plane + zoff) = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   // standard binary masks, as cim_bwd_gx_v8_kernel, now summed over k for each a-slice j: the
   // plain mask (cD_kj = 2^(bsa*j)) gives D_j = 2^(bsa*j) * popcount(pass bits of slice j); the
@@ -510,12 +516,25 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   struct Pref {
     XW w[2][10];
   };
+  // a stage's first pixel m0 = 128 s (M < 2^31): image b0 and, when a stage is part of one image,
+  // its first staged input row; per-thread staging items are stage-invariant (decomposed once)
   auto stage_geom = [&](int stg, int& b0, int& ih_first) {
-    const size_t m0 = ((size_t)chunk * v.nstage + stg) * 128;
-    b0 = (int)(m0 / g.P);
-    const int pim0 = (int)(m0 - (size_t)b0 * g.P);
+    const unsigned m0 = (unsigned)(chunk * v.nstage + stg) * 128u;
+    b0 = (int)(m0 / (unsigned)g.P);
+    const int pim0 = (int)(m0 - (unsigned)b0 * (unsigned)g.P);
     ih_first = v.whole ? 0 : (pim0 >> v.lw) * SS - g.PH;
   };
+  int it_cl[2], it_db[2], it_ih[2], it_c8[2];
+#pragma unroll
+  for (int u2 = 0; u2 < 2; ++u2) {
+    const int it = threadIdx.x + u2 * 256;
+    const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
+    const int slot = rem >> (v.lw - 3), c8 = rem & (ng8 - 1);
+    it_cl[u2] = cl;
+    it_c8[u2] = c8;
+    it_db[u2] = v.whole ? slot / g.H : 0;
+    it_ih[u2] = v.whole ? slot - it_db[u2] * g.H : slot;
+  }
   auto load = [&](int stg, Pref& pf) {
     if (SS != 1) return;  // stride 2 stages without prefetch (17 source words per item)
     int b0, ih_first;
@@ -526,10 +545,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
       for (int u = 0; u < 10; ++u) pf.w[u2][u] = xzero<XW>();
       if (it < nit) {
-        const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
-        const int slot = rem / ng8, c8 = rem - slot * ng8;
-        int b = b0, ih = ih_first + slot;
-        if (v.whole) { b = b0 + slot / g.H; ih = slot - (slot / g.H) * g.H; }
+        const int cl = it_cl[u2], c8 = it_c8[u2];
+        const int b = b0 + it_db[u2], ih = ih_first + it_ih[u2];
         const int c = cb * 16 + cl;
         if (c < g.C && ih >= 0 && ih < g.H && b < g.B) {
           const XW* src = reinterpret_cast<const XW*>(xcb) + (((size_t)b * g.C + c) * g.H + ih) * g.W + c8 * 8;
@@ -541,11 +558,59 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     }
   };
 
+  // stride 2 keeps the per-stage LDS reduction: the registers would cost it a wave per SIMD
+  constexpr bool RGQ = !PLS && SS == 1;
+  constexpr int NGQ = RGQ ? NKJ : 1;
+  float gq0[NGQ], gq1[NGQ];  // grad_alpha partials of tiles i_lo, i_lo + 1 (this lane's pixels)
+#pragma unroll
+  for (int kj = 0; kj < NGQ; ++kj) gq0[kj] = gq1[kj] = 0.f;
   Pref pf;
   load(0, pf);
   for (int stg = 0; stg < v.nstage; ++stg) {
     int b0, ih_first;
     stage_geom(stg, b0, ih_first);
+    // this wave's K-step: pixels mk .. mk+31; this lane's 8 pixels mk8 .. mk8+7 (one row).  Its
+    // grad_out and the state words of the first two tiles are loaded here, ahead of the staging,
+    // so that their latency hides behind it
+    const size_t mk8 = ((size_t)chunk * v.nstage + stg) * 128 + 32 * wave + 8 * g4;
+    const bool kvalid = mk8 < (size_t)g.M;
+    // image and in-image pixel: a stage lies in one image, or (whole) spans 128 / P images of a
+    // power-of-two P
+    int b = b0, pimg;
+    {
+      const int moff = 32 * wave + 8 * g4;
+      if (v.whole) {
+        const int lp = __builtin_ctz(g.P);
+        b = b0 + (moff >> lp);
+        pimg = moff & (g.P - 1);
+      } else {
+        pimg = (int)((unsigned)(chunk * v.nstage + stg) * 128u - (unsigned)b0 * (unsigned)g.P) + moff;
+      }
+    }
+    const int oh = pimg >> v.lw, ow0 = pimg & (Wo - 1);
+    float gv[8];
+    uint32_t sv0[8], sv1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gv[e] = 0.f; sv0[e] = sv1[e] = 0u; }
+    if (kvalid) {
+      if (g.onchw) {
+        const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
+        const float4 a0 = gp[0], a1 = gp[1];
+        gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
+        gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] = gout[(mk8 + e) * g.O + o];
+      }
+      if (!PLS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv0[e] = st[((size_t)i_lo * g.M + mk8 + e) * g.O + o];
+        if (ntl > 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sv1[e] = st[((size_t)(i_lo + 1) * g.M + mk8 + e) * g.O + o];
+        }
+      }
+    }
     __syncthreads();
     if (SS == 2) {
       // stride 2: output column ow reads input column 2 ow + kw - 1 -> 17 words per 8 columns
@@ -590,8 +655,8 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #else
       if (it < nit) {
 #endif
-        const int cl = it / (v.NSLOT * ng8), rem = it - cl * (v.NSLOT * ng8);
-        const int slot = rem / ng8, c8 = rem - slot * ng8;
+        const int cl = it_cl[u2], c8 = it_c8[u2];
+        const int slot = v.whole ? it_db[u2] * g.H + it_ih[u2] : it_ih[u2];
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
 #pragma unroll
@@ -611,22 +676,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     }
     __syncthreads();
     if (stg + 1 < v.nstage) load(stg + 1, pf);
-    // this wave's K-step: pixels mk .. mk+31; this lane's 8 pixels mk8 .. mk8+7 (one row)
-    const size_t mk8 = ((size_t)chunk * v.nstage + stg) * 128 + 32 * wave + 8 * g4;
-    if (mk8 >= (size_t)g.M) continue;
-    const int b = (int)(mk8 / g.P);
-    const int pimg = (int)(mk8 - (size_t)b * g.P);
-    const int oh = pimg >> v.lw, ow0 = pimg & (Wo - 1);
-    float gv[8];
-    if (g.onchw) {
-      const float4* gp = reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + pimg);
-      const float4 a0 = gp[0], a1 = gp[1];
-      gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
-      gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gv[e] = gout[(mk8 + e) * g.O + o];
-    }
+    if (!kvalid) continue;
     // row slot of each kernel row for this lane's output row (-1: outside the image)
     int slot_kh[3];
 #pragma unroll
@@ -719,30 +769,34 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             const int kh = gpk[gr] & 3;
             const int sl = kh == 0 ? slot_kh[0] : (kh == 1 ? slot_kh[1] : slot_kh[2]);
             const bool ok = gpk[gr] >= 0 && sl >= 0;
-            const __bf16* src = pl + (size_t)j * 3 * CPL * v.CPITCH + (ok ? (gpk[gr] >> 2) + sl * Wo : 0) + ow0;
-            v4i a4 = *reinterpret_cast<const v4i*>(src);
-            a4 = ok ? a4 : v4i{0, 0, 0, 0};
-            const v8bf a = as_v8bf(a4);
+            const __bf16* src = pl + (size_t)j * 3 * plane + (ok ? (gpk[gr] >> 2) + sl * Wo + ow0 : zoff);
+            const v8bf a = as_v8bf(*reinterpret_cast<const v4i*>(src));
 #ifndef CIMQ_EXP_GW_NOMFMA
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[gr], 0, 0, 0);
 #else
-            acc[gr][0] += (float)a4[0] + (float)bh[0] + (float)bm[1] + (float)bq[2];
+            acc[gr][0] += (float)a[0] + (float)bh[0] + (float)bm[1] + (float)bq[2];
 #endif
           }
         }
       } else if (!PLS && tl < ntl) {
         const int i = i_lo + tl;
         uint32_t sv[8];
+        if (tl < 2) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
+          for (int e = 0; e < 8; ++e) sv[e] = tl == 0 ? sv0[e] : sv1[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
+        }
         // grad_alpha partials (lsq.py:321-333): sum over the pixels of code * g
 #ifdef CIMQ_EXP_GW_NOGA
         if (false) {
 #else
         if (((i * g.xbar) / KHW) / 16 == cb) {
 #endif
+          float qv[NKJ];
 #pragma unroll
           for (int kj = 0; kj < NKJ; ++kj) {
             float q = 0.f;
@@ -753,9 +807,24 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
               const int code = ((int)(sv[e] << (29 - 3 * kj))) >> 30;
               q = __builtin_fmaf((float)code, gv[e], q);
             }
-            q += __shfl_xor(q, 16);
-            q += __shfl_xor(q, 32);
-            if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
+            qv[kj] = q;
+          }
+          // the first two tiles accumulate per lane in registers over the chunk (one cross-lane
+          // reduction at the end); a third takes the per-stage reduction into LDS
+          if (RGQ && tl == 0) {
+#pragma unroll
+            for (int kj = 0; kj < NGQ; ++kj) gq0[kj] += qv[kj];
+          } else if (RGQ && tl == 1) {
+#pragma unroll
+            for (int kj = 0; kj < NGQ; ++kj) gq1[kj] += qv[kj];
+          } else {
+#pragma unroll
+            for (int kj = 0; kj < NKJ; ++kj) {
+              float q = qv[kj];
+              q += __shfl_xor(q, 16);
+              q += __shfl_xor(q, 32);
+              if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
+            }
           }
         }
         // B operands: g * D_j, D_j = sum_k cD_kj * pass_ijk, split into bf16 hi / mid / lo
@@ -777,18 +846,15 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           }
           split3x8(d, bh[j], bm[j], bq[j]);
         }
-        // A fragments of a row group (rows past C and kernel rows outside the image are zeroed by
-        // a select, no branch)
+        // A fragments of a row group (rows past C and kernel rows outside the image read the
+        // zero pad: one address select, no branch)
         auto read_group = [&](int gr, v4i (&dst)[NBA]) {
           const int kh = gpk[gr] & 3;
           const int sl = kh == 0 ? slot_kh[0] : (kh == 1 ? slot_kh[1] : slot_kh[2]);
           const bool ok = gpk[gr] >= 0 && sl >= 0;
-          const __bf16* src = pl + (ok ? (gpk[gr] >> 2) + sl * Wo : 0) + ow0;
+          const __bf16* src = pl + (ok ? (gpk[gr] >> 2) + sl * Wo + ow0 : zoff);
 #pragma unroll
-          for (int j = 0; j < NBA; ++j) {
-            const v4i a = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * CPL * v.CPITCH);
-            dst[j] = ok ? a : v4i{0, 0, 0, 0};
-          }
+          for (int j = 0; j < NBA; ++j) dst[j] = *reinterpret_cast<const v4i*>(src + (size_t)j * 3 * plane);
         };
 #pragma unroll
         for (int gr = 0; gr < NGR; ++gr) {
@@ -806,6 +872,22 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #else
           acc[gr][0] += (float)acur[0][0];
 #endif
+        }
+      }
+    }
+  }
+  if (RGQ) {
+    // the register grad_alpha partials of the first two tiles into this wave's LDS region
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+      const int i = i_lo + tl;
+      if (tl < ntl && ((i * g.xbar) / KHW) / 16 == cb) {
+#pragma unroll
+        for (int kj = 0; kj < NGQ; ++kj) {
+          float q = tl == 0 ? gq0[kj] : gq1[kj];
+          q += __shfl_xor(q, 16);
+          q += __shfl_xor(q, 32);
+          if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
         }
       }
     }
