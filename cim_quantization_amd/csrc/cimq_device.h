@@ -4,6 +4,12 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
+
+// every kernel's lane math (16-lane MFMA rows, xor-32 butterflies, threadIdx >> 6 wave ids)
+// assumes 64-lane wavefronts (CDNA)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "libcimq assumes 64-lane wavefronts (gfx9 CDNA targets)"
+#endif
 #include <stdint.h>
 
 // The kernels assume 64-lane waves (shuffle butterflies over 32..1, threadIdx >> 6 as the

@@ -79,20 +79,10 @@ __device__ inline void act_item(const Geo& g, const float* __restrict__ x, float
 // NBA_C > 0: nba = NBA_C and bsa = 1 at compile time (the unrolled digit loop has no runtime
 // bounds); 0: read from g
 template <int NBP, int NBA_C = 0>
-__device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint32_t (&fwd)[NBP / 4],
-                                 uint32_t (&bwd)[NBP / 4]) {
+__device__ inline void act_words_xq(const Geo& g, float xq, float sa, bool sgn, uint32_t (&fwd)[NBP / 4],
+                                    uint32_t (&bwd)[NBP / 4]) {
   const int nba = NBA_C > 0 ? NBA_C : g.nba;
   const int bsa = NBA_C > 0 ? 1 : g.bsa;
-  float xq;
-  if (g.input_kind == 1) {
-    const float t = v / sa;
-    const float c = clamp_nan(t, 0.f, g.lsq_qp);
-    const float r = rintf(c);
-    const float rp = (r - c) + c;  // round_pass value
-    xq = rp * sa;
-  } else {
-    xq = v;
-  }
   const float xi = xq / sa;
   const int xhi = to_i8_wrap(xi);
   const int mask = (1 << bsa) - 1;
@@ -133,10 +123,71 @@ __device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint
   }
 }
 
+// x_q of one element: with RAW_LSQ the activation quantiser round_pass(clamp(x/sa,0,Qp))*sa
+// (lsq.py:549), else the input itself
+__device__ inline float act_xq(const Geo& g, float v, float sa) {
+  if (g.input_kind != 1) return v;
+  const float t = v / sa;
+  const float c = clamp_nan(t, 0.f, g.lsq_qp);
+  const float r = rintf(c);
+  const float rp = (r - c) + c;  // round_pass value
+  return rp * sa;
+}
+
+template <int NBP, int NBA_C = 0>
+__device__ inline void act_words(const Geo& g, float v, float sa, bool sgn, uint32_t (&fwd)[NBP / 4],
+                                 uint32_t (&bwd)[NBP / 4]) {
+  act_words_xq<NBP, NBA_C>(g, act_xq(g, v, sa), sa, sgn, fwd, bwd);
+}
+
+// RAW_LSQ: the words depend on the element only through the integer code r = rint(clamp(x/sa,
+// 0, Qp)) -- round_pass gives rp = (r - c) + c = r exactly for c in [0, Qp], so x_q = r * sa --
+// so a block tabulates the Qp + 1 words once (with the same act_words_xq) and each element
+// takes the quantiser's division, clamp and rint, then a table lookup; a NaN code (NaN input)
+// takes the element-wise chain.  lut: [Qp + 1][fwd words, bwd words] in LDS.
+constexpr int kActLutMax = 256;
+template <int NBP, int NBA_C>
+__device__ inline void act_lut_build(const Geo& g, float sa, bool sgn, uint32_t* lut) {
+  const int nl = (int)g.lsq_qp + 1;
+  for (int r = threadIdx.x; r < nl; r += blockDim.x) {
+    uint32_t f[NBP / 4], b[NBP / 4];
+    act_words_xq<NBP, NBA_C>(g, (float)r * sa, sa, sgn, f, b);
+#pragma unroll
+    for (int w = 0; w < NBP / 4; ++w) {
+      lut[r * (NBP / 2) + w] = f[w];
+      lut[r * (NBP / 2) + NBP / 4 + w] = b[w];
+    }
+  }
+  __syncthreads();
+}
+template <int NBP, int NBA_C>
+__device__ inline void act_words_lut(const Geo& g, float v, float sa, bool sgn, const uint32_t* lut,
+                                     uint32_t (&fwd)[NBP / 4], uint32_t (&bwd)[NBP / 4]) {
+  const float c = clamp_nan(v / sa, 0.f, g.lsq_qp);
+  const float r = rintf(c);
+  if (r == r) {
+    const int e = (int)r * (NBP / 2);
+    if (NBP == 4) {
+      const uint2 t = *reinterpret_cast<const uint2*>(lut + e);
+      fwd[0] = t.x;
+      bwd[0] = t.y;
+    } else {
+      const uint4 t = *reinterpret_cast<const uint4*>(lut + e);
+      fwd[0] = t.x;
+      fwd[NBP / 4 - 1] = t.y;
+      bwd[0] = t.z;
+      bwd[NBP / 4 - 1] = t.w;
+    }
+  } else {
+    act_words<NBP, NBA_C>(g, v, sa, sgn, fwd, bwd);
+  }
+}
+
 // four consecutive elements (idx4 = 4 * t): one 16-B load, 16-B (NBP 4) or 2 x 16-B stores
 template <int NBP, int NBA_C = 0>
 __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
-                                 uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long t) {
+                                 uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long t,
+                                 const uint32_t* lut = nullptr) {
   const float4 v4 = reinterpret_cast<const float4*>(x)[t];
   const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
   uint32_t f[4][NBP / 4], b[4][NBP / 4];
@@ -146,8 +197,13 @@ __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, floa
 #pragma unroll
     for (int w = 0; w < NBP / 4; ++w) f[e][w] = b[e][w] = __float_as_uint(vv[e]);
 #else
+  if (lut) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) act_words<NBP, NBA_C>(g, vv[e], sa, sgn, f[e], b[e]);
+    for (int e = 0; e < 4; ++e) act_words_lut<NBP, NBA_C>(g, vv[e], sa, sgn, lut, f[e], b[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) act_words<NBP, NBA_C>(g, vv[e], sa, sgn, f[e], b[e]);
+  }
 #endif
   if (NBP == 4) {
     reinterpret_cast<uint4*>(xcf)[t] = make_uint4(f[0][0], f[1][0], f[2][0], f[3][0]);
@@ -161,21 +217,33 @@ __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, floa
 }
 
 // all elements of x: vectorised when Nin % 4 == 0 (W % 4 == 0), element-wise otherwise
+template <int NBP, int NBA_C>
+__device__ inline void act_range_sel(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
+                                     uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long first,
+                                     long long step, uint32_t* lut) {
+  const long long n4 = g.Nin / 4;
+  const bool tab = lut && g.input_kind == 1 && g.lsq_qp >= 0.f && g.lsq_qp < (float)kActLutMax;
+  if (tab) act_lut_build<NBP, NBA_C>(g, sa, sgn, lut);  // block-uniform condition: every thread syncs
+  for (long long t = first; t < n4; t += step) act_item4<NBP, NBA_C>(g, x, sa, sgn, xcf, xcb, t, tab ? lut : nullptr);
+}
+
+// lut: LDS for the RAW_LSQ word table (kActLutMax * NBP / 2 words), or null; called by every
+// thread of the block
 __device__ inline void act_range(const Geo& g, const float* __restrict__ x, float sa, bool sgn,
                                  uint8_t* __restrict__ xcf, uint8_t* __restrict__ xcb, long long first,
-                                 long long step) {
+                                 long long step, uint32_t* lut = nullptr) {
   if (g.Nin % 4 == 0) {
     const long long n4 = g.Nin / 4;
     // the 1-bit-slice cases of the CIFAR / QuantLinear configs with compile-time digit loops
     const int sel = g.bsa != 1 ? 0 : g.nba;
     if (sel == 3)
-      for (long long t = first; t < n4; t += step) act_item4<4, 3>(g, x, sa, sgn, xcf, xcb, t);
+      act_range_sel<4, 3>(g, x, sa, sgn, xcf, xcb, first, step, lut);
     else if (sel == 2)
-      for (long long t = first; t < n4; t += step) act_item4<4, 2>(g, x, sa, sgn, xcf, xcb, t);
+      act_range_sel<4, 2>(g, x, sa, sgn, xcf, xcb, first, step, lut);
     else if (sel == 4)
-      for (long long t = first; t < n4; t += step) act_item4<4, 4>(g, x, sa, sgn, xcf, xcb, t);
+      act_range_sel<4, 4>(g, x, sa, sgn, xcf, xcb, first, step, lut);
     else if (sel == 8)
-      for (long long t = first; t < n4; t += step) act_item4<8, 8>(g, x, sa, sgn, xcf, xcb, t);
+      act_range_sel<8, 8>(g, x, sa, sgn, xcf, xcb, first, step, lut);
     else if (g.NBP == 4)
       for (long long t = first; t < n4; t += step) act_item4<4>(g, x, sa, sgn, xcf, xcb, t);
     else

@@ -144,8 +144,9 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
     const float sa = grad_scale_value(a.alpha_act[0], q.gs_a);  // lsq.py:547-548
     const int ab = (int)blockIdx.x - nwblk;
     const bool sgn = a.signed_act[0] != 0.f;
+    __shared__ __attribute__((aligned(16))) uint32_t lut[kActLutMax * 4];  // the RAW_LSQ word table (act_range)
     act_range(g, a.x, sa, sgn, a.xcf, a.xcb, (long long)ab * blockDim.x + threadIdx.x,
-              (long long)a.nact_blocks * blockDim.x);
+              (long long)a.nact_blocks * blockDim.x, lut);
     return;
   }
 #ifdef CIMQ_EXP_PREP_NOWT

@@ -13,4 +13,7 @@ cp $O/kt/p_kernel_stats.csv $O/kernel_stats.csv
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o p -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-cfg5 --no-graph > $O/pmc_f.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w -o p -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-cfg5 --no-graph > $O/pmc_w.log 2>&1 || exit 1
 python tools/pmc_traffic.py $O/pmc_f/p_counter_collection.csv $O/pmc_w/p_counter_collection.csv > $O/pmc_traffic.json
+# the bench line again, its roofline.traffic read from the passes just taken (same sources)
+CIMQ_TRAFFIC_JSON=$O/pmc_traffic.json timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_with_traffic.json 2> $O/bench_with_traffic.err || exit 1
+python tools/step_breakdown.py $O/kt/p_kernel_trace.csv > $O/step_breakdown.txt
 echo done
