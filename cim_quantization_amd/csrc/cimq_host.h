@@ -285,7 +285,7 @@ inline Plan3 v3_plan(const Geo& g) {
   const size_t fwd_common = patch + (size_t)g.T * g.KS * 64 * 4 + ckl;
   const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * (16 + 4);
   const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
-  v.fwd_res = fwd_res <= 80 * 1024 ? 1 : 0;
+  v.fwd_res = fwd_res <= (size_t)tune("FWD_RES_KB", 52) * 1024 ? 1 : 0;
   p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
   p.lds_gx = a16((size_t)3 * (v.NPB + 1) * 32 * 2) + a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + ckl + 64;
   {
