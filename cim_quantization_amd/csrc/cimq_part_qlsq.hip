@@ -20,6 +20,8 @@ struct LsqQ {
   long long n;
   float qn, qp;
   int scaled;  // LinearLSQ: the quantised value times s (lsq.py:611); else the integer code
+  int vec;     // x and out 16-byte aligned: float4 loads / stores (else element-wise: a parameter
+               // view inside a flat buffer, a batch slice, sits at any 4-byte offset)
 };
 
 __device__ inline float lsq_code(float x, float s, float qn, float qp) {
@@ -29,7 +31,7 @@ __device__ inline float lsq_code(float x, float s, float qn, float qp) {
 __global__ __launch_bounds__(256) void lsq_quant_fwd_kernel(LsqQ q, const float* __restrict__ x,
                                                             const float* __restrict__ s_p, float* __restrict__ out) {
   const float s = *s_p;
-  const long long n4 = q.n >> 2;
+  const long long n4 = q.vec ? q.n >> 2 : 0;
   const long long step = (long long)gridDim.x * blockDim.x;
   for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += step) {
     const float4 v = reinterpret_cast<const float4*>(x)[t];
@@ -332,9 +334,10 @@ int cimq_lsq_quantize_forward(const float* x, long long n, const float* s, float
                               float* out, void* stream) {
   if (n < 0 || (n > 0 && (!x || !s || !out))) return fail(CIMQ_EINVAL, "lsq_quantize_forward: bad arguments");
   if (n == 0) return CIMQ_OK;
-  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15)
-    return fail(CIMQ_EINVAL, "lsq_quantize_forward: x / out must be 16-byte aligned");
-  LsqQ q{n, qn, qp, scaled ? 1 : 0};
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 3)
+    return fail(CIMQ_EINVAL, "lsq_quantize_forward: x / out must be float-aligned");
+  const int vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15) ? 0 : 1;
+  LsqQ q{n, qn, qp, scaled ? 1 : 0, vec};
   hipLaunchKernelGGL(lsq_quant_fwd_kernel, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, q, x, s, out);
   return check_hip("lsq_quant_fwd");
 }
@@ -346,7 +349,7 @@ int cimq_lsq_quantize_backward(const float* x, long long n, const float* s, floa
   hipStream_t st = (hipStream_t)stream;
   const int nb = ew_blocks(n);
   float* part = reinterpret_cast<float*>(ws);
-  LsqQ q{n, qn, qp, scaled ? 1 : 0};
+  LsqQ q{n, qn, qp, scaled ? 1 : 0, 0};
   if (n > 0) {
     hipLaunchKernelGGL(lsq_quant_bwd_kernel, dim3(nb), dim3(256), 0, st, q, x, s, grad_out, grad_x, part);
     CIMQ_TRY(check_hip("lsq_quant_bwd"));

@@ -180,6 +180,12 @@ class FlatSGD:
 
     @torch.no_grad()
     def step(self):
+        """One update from the bucket's gradients.  Every parameter takes part (a parameter that
+        got no gradient this step updates from a zero gradient -- momentum and weight decay still
+        apply -- where torch.optim.SGD would skip it; the CiM training step gives every parameter
+        a gradient).  Gradients autograd left outside the bucket are copied in first."""
+        self.bucket.join()
+        self.bucket.sync_views()
         d = torch.addcmul(self.bucket.flat, self.wd, self.flat)  # g + wd * p
         if self.started:
             self.buf.mul_(self.momentum).add_(d)

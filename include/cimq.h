@@ -264,7 +264,7 @@ int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* cod
 /* ---- plain LSQ modules (lsq.py:389-436 Conv2dLSQ, :591-617 LinearLSQ, :620-662 ActLSQ) ---- */
 
 /* The LSQ quantiser out = round_pass(clamp(x / s, qn, qp)) [* s if scaled] over n fp32
- * elements (x, out 16-byte aligned), s = *s the grad-scaled step size (grad_scale(alpha, g),
+ * elements (any float-aligned x, out: 16-byte aligned ones take vector loads), s = *s the grad-scaled step size (grad_scale(alpha, g),
  * lsq.py:407-412 / :608-611 / :653-656, evaluated by the caller).  Replaces those lines'
  * torch ops: ActLSQ's codes (scaled = 0), Conv2dLSQ's weight codes (0), LinearLSQ's w_q (1). */
 int cimq_lsq_quantize_forward(const float* x, long long n, const float* s, float qn, float qp, int scaled,

@@ -110,3 +110,45 @@ def test_quantiser_ties_and_clamp(cuda_device):
     for scaled in (False, True):
         out = lsq_quantize(torch.from_numpy(x).to(cuda_device), st, -4, 3, scaled=scaled).cpu().numpy()
         np.testing.assert_array_equal(out, po.lsq_forward(x, s, -4, 3, scaled=scaled))
+
+
+def test_plain_modules_with_flat_params(cuda_device):
+    """Parameters inside dist.FlatSGD's flat buffer sit at arbitrary 4-byte offsets (a 432-element
+    conv weight plus a 1-element alpha put the next weight at byte 1732), and so does a batch
+    slice of a flat activation buffer: the quantiser takes them element-wise, same results."""
+    import copy
+
+    from cim_quantization_amd._modules.lsq import ActLSQ, Conv2dLSQ, LinearLSQ
+    from cim_quantization_amd.dist import FlatSGD, GradBucket
+    dev = cuda_device
+    torch.manual_seed(3)
+    mods = [ActLSQ(nbits_a=4), Conv2dLSQ(3, 16, 3, padding=1, bias=False, nbits_w=4), LinearLSQ(576, 10, nbits_w=4)]
+    refs = copy.deepcopy(mods)
+    mods = [m.to(dev).train() for m in mods]
+    refs = [m.to(dev).train() for m in refs]
+    bucket = GradBucket([p for m in mods for p in m.parameters()])
+    opt = FlatSGD(bucket, lr=0.05, momentum=0.9)
+    assert mods[2].weight.data_ptr() % 16 != 0  # the case the 16-byte-only quantiser refused
+    buf = torch.randn(1 + 4 * 3 * 6 * 6, device=dev).relu()
+    x = buf[1:].view(4, 3, 6, 6)  # misaligned activation
+    xr = x.clone()
+    g = torch.randn(4, 10, device=dev)
+    for step in range(2):
+        bucket.zero()
+        for m in refs:
+            for p in m.parameters():
+                p.grad = None
+        y = mods[2](mods[1](mods[0](x)).flatten(1))
+        yr = refs[2](refs[1](refs[0](xr)).flatten(1))
+        assert torch.equal(y, yr)
+        y.backward(g)
+        yr.backward(g)
+        bucket.exchange()
+        for m, r in zip(mods, refs):
+            for (n, p), pr in zip(m.named_parameters(), r.parameters()):
+                assert torch.equal(p.grad, pr.grad), n
+        opt.step()
+        with torch.no_grad():  # the same SGD step on the reference copies
+            for m, r in zip(mods, refs):
+                for p, pr in zip(m.parameters(), r.parameters()):
+                    pr.copy_(p)
