@@ -383,8 +383,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
+        # "nccl" is RCCL on ROCm (one GPU per rank); CIMQ_DIST_BACKEND=gloo runs the same branch with
+        # several ranks on one GPU (tests/test_gpu_dist.py)
+        dist.init_process_group(os.environ.get("CIMQ_DIST_BACKEND", "nccl"), rank=rank, world_size=world)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
 
     from cim_quantization_amd import _lib
