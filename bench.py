@@ -283,13 +283,19 @@ def cpu_baseline(batch_cpu: int, threads: int):
 
 def bench_cfg5(dev, steps, warmup):
     """BASELINE cfg5: QuantLinear 1024->1024 w4a4, 128-row tiles, batch 4096, as Conv2dLSQCiM(k=1)
-     through the module path: fwd+bwd ms per step and forward MAC/s."""
+     through the module path (the dense GEMM kernels, cimq_part_dense.hip): fwd+bwd
+    ms per step, forward MAC/s, and the roofline of each of its three kernels (HIP events around
+    every launch; bound = the larger of the HBM time of the algorithmic bytes and the MFMA time of
+    the products as issued: int8 bit-slice products forward, three bf16 products per fp32-accurate
+    backward MAC)."""
     import cim_quantization_amd._modules as my_nn
+    from cim_quantization_amd import _lib
     torch.manual_seed(7)
-    m = my_nn.Conv2dLSQCiM(1024, 1024, 1, 1, 0, bias=False, nbits_w=4, nbits_a=4, nbits_alpha=8, wbitslice=1,
+    B, C, O, nb = 4096, 1024, 1024, 4
+    m = my_nn.Conv2dLSQCiM(C, O, 1, 1, 0, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
                            abitslice=1, xbar=128, adcbits=1.5).to(dev).train()
-    x = torch.randn(4096, 1024, 1, 1, device=dev).relu()
-    gy = torch.randn(4096, 1024, 1, 1, device=dev) / 2048.0
+    x = torch.randn(B, C, 1, 1, device=dev).relu()
+    gy = torch.randn(B, O, 1, 1, device=dev) / 2048.0
     for _ in range(max(1, warmup)):
         m(x).backward(gy)
     torch.cuda.synchronize(dev)
@@ -304,9 +310,30 @@ def bench_cfg5(dev, steps, warmup):
             m(x)
         torch.cuda.synchronize(dev)
     fw = (time.perf_counter() - t0) / steps
-    macs = 4096 * 1024 * 1024
+    macs = B * O * C
+    roofs = {}
+    for kname, ops_per_mac, peak, unit in (("fwd", 2.0 * nb * nb, PEAK_I8_TOPS, "TOP/s"),
+                                           ("bwd_gx", 3.0 * 2 * nb, PEAK_BF16_TFLOPS, "TFLOP/s"),
+                                           ("bwd_gw", 3.0 * 2 * nb, PEAK_BF16_TFLOPS, "TFLOP/s")):
+        with _lib.KernelTimer(kname, max_launches=steps + 4) as kt:
+            for _ in range(steps):
+                m(x).backward(gy)
+            torch.cuda.synchronize(dev)
+        n = max(kt.launches, 1)
+        avg = kt.total_ms / n * 1e-3
+        byts = kt.algo_bytes / n
+        t_hbm = byts / (PEAK_HBM_GBS * 1e9)
+        ops = macs * ops_per_mac
+        t_mfma = ops / (peak * 1e12)
+        r = ({"bound": "hbm", "achieved": byts / avg / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s"} if t_hbm >= t_mfma
+             else {"bound": "mfma", "achieved": ops / avg / 1e12, "peak": peak, "unit": unit})
+        r.update(frac=r["achieved"] / r["peak"], avg_launch_us=avg * 1e6, t_hbm_us=t_hbm * 1e6, t_mfma_us=t_mfma * 1e6)
+        roofs[kname] = r
+    dom = max(roofs, key=lambda k: roofs[k]["avg_launch_us"])
     return {"workload": "quantlinear_1024x1024_w4a4_xbar128_b4096", "ms_fwd_bwd": fb * 1e3, "ms_fwd": fw * 1e3,
-            "fwd_mac_per_s": macs / fw, "fwd_bwd_mac_per_s": macs / fb, "launch": "eager"}
+            "fwd_mac_per_s": macs / fw, "fwd_bwd_mac_per_s": macs / fb, "launch": "eager",
+            "roofline": dict(roofs[dom], kernel=dom, traffic=None), "kernel_roofs": roofs,
+            "reference_cpu_container_ms": {"fwd": 2420.0, "fwd_bwd": 45940.0}}
 
 
 def resnet56_convs():

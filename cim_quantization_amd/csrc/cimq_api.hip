@@ -78,6 +78,10 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
     return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
   }
   if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
+  if (dense_plan(g)) {
+    *lsq_fused = false;
+    return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s);
+  }
   return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
 }
 
@@ -449,6 +453,7 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
     g.onchw = 1;
     return launch_fwd_any(g, c, scal + 1, scal, out, nullptr, nullptr, s);
   }
+  if (dense_plan(g)) return launch_fwd_any(g, c, scal + 1, scal, out, nullptr, nullptr, s);  // P = 1: NCHW is [B, P, O]
   // general kernels write [B, P, O]; the module returns NCHW
   WsLayout W = ws_layout(g);
   float* bpo = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + W.bpo);
@@ -495,7 +500,7 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   const float* gsrc = grad_out;
   if (p.ok) {
     g.onchw = 1;
-  } else {
+  } else if (!dense_plan(g)) {  // (P = 1: NCHW grad_out is already [B, P, O])
     float* bpo = reinterpret_cast<float*>(w + W.bpo);
     hipLaunchKernelGGL(nchw_to_bpo_kernel, dim3(std::min(cdiv((long long)g.M * g.O, 256), 8192)), dim3(256), 0, s,
                        g, grad_out, bpo);

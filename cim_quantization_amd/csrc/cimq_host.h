@@ -149,6 +149,8 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 // parameters, the module's step sizes -- functions of the parameters only, so a prepared
 // buffer (cimq_module_prepare, cimq_lsq_desc.wprep) can hold them instead), then the
 // activation-side regions (slice words, state words) of one forward.
+inline bool dense_plan(const Geo& g);
+
 struct CtxLayout {
   size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
@@ -181,7 +183,10 @@ inline CtxLayout ctx_layout(const Geo& g) {
   // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
   // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three
   // 64-bit planes for w8a8) per (tile, pixel, channel)
-  L.st = o; o = align256(o + std::max((size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4), (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24)));
+  // (the dense path, cimq_part_dense.hip: a uint2 of three 16-bit planes per (i, m, o))
+  L.st = o; o = align256(o + std::max({(size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4),
+                                       (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24),
+                                       dense_plan(g) ? (size_t)g.T * g.M * g.O * 8 : (size_t)0}));
   L.total = o;
   return L;
 }
@@ -408,6 +413,26 @@ inline Plan7 v7_plan(const Geo& g) {
   return p;
 }
 
+// ---- the dense path (cimq_part_dense.hip): 1x1 kernels on 1x1 images, a [B][C] x [C][O] GEMM ----
+// (BASELINE cfg5, QuantLinear as Conv2dLSQCiM(k=1) on [B, C, 1, 1]); the library ternary ADC, equal
+// weight / activation slice counts up to 4 (the uint2 state word holds 16 slice pairs per plane)
+inline bool dense_plan(const Geo& g) {
+  if (tune("DENSE", 1) == 0) return false;
+  if (g.KH != 1 || g.KW != 1 || g.SH != 1 || g.SW != 1 || g.PH != 0 || g.PW != 0 || g.H != 1 || g.W != 1) return false;
+  if (g.variant != VAR_LIBRARY || g.mode != ADC_TERNARY || g.NBP != 4 || g.nbw != g.nba || g.nbw > 4) return false;
+  if (g.xbar % 64 != 0 || g.C % 16 != 0 || g.O % 64 != 0 || g.M % 128 != 0) return false;
+  return true;
+}
+// grad_w row chunks: about 512 workgroups over (chunks x tiles x 64-channel groups), 32-row multiples
+inline int dense_chunks(const Geo& g) {
+  const int per = std::max(1, 512 / (g.T * (g.O / 64)));
+  return std::max(1, std::min(per, g.M / 256));
+}
+inline int dense_rows_per_chunk(const Geo& g) {
+  const int n = dense_chunks(g);
+  return ((g.M + n - 1) / n + 31) / 32 * 32;
+}
+
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, lsq_part, gaq, wpart, bpo, total;
   int rows, nchunks, nchunks_bwd;
@@ -419,7 +444,7 @@ inline WsLayout ws_layout(const Geo& g) {
   // backward slabs: the v7 grad_w kernel's pixel chunks when it applies (the alpha_cim init
   // kernel keeps gw_chunks' split: W.nchunks / W.rows)
   const Plan7 p7 = v7_plan(g);
-  W.nchunks_bwd = p7.ok ? p7.v.nchunks : W.nchunks;
+  W.nchunks_bwd = p7.ok ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
   const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
@@ -520,6 +545,10 @@ inline void prof_end(int slot, hipStream_t s) {
 // the general kernel with ps_dbg / adc_dbg also writes every partial sum and ADC output)
 int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
                    float* adc_dbg, hipStream_t s);
+// cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
+int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
+int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
+                     hipStream_t s);
 // cimq_part_bwd.hip: backward of layers outside the v7 plan (v5 / v6 and general kernels)
 int launch_bwd_general(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                        const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused);

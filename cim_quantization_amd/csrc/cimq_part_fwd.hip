@@ -67,6 +67,12 @@ int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, flo
 
 int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
                    float* adc_dbg, hipStream_t s) {
+  if (dense_plan(g)) {
+    // the dense GEMM path (its state words feed the dense backward); the debug hook then reruns
+    // the general kernel for the partial sums (same out values)
+    CIMQ_TRY(launch_dense_fwd(g, ctx, sw, sa, out, s));
+    if (!ps_dbg) return CIMQ_OK;
+  }
   if (ps_dbg) {
     if (g.NBP == 4) return launch_fwd<4, true>(g, ctx, sw, sa, out, ps_dbg, adc_dbg, s);
     return launch_fwd<8, true>(g, ctx, sw, sa, out, ps_dbg, adc_dbg, s);

@@ -116,6 +116,11 @@ RANDOM_CASES = [
     dict(B=2, C=3, O=16, H=32, k=3, s=1, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=1),
     dict(B=2, C=3, O=16, H=16, k=3, s=2, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=1),
     dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=8, ab=8, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    # the dense GEMM path (1x1 kernels on 1x1 images, cimq_part_dense.hip): 16 / 4 / 9 slice pairs, a
+    # partial last tile, signed activations
+    dict(B=128, C=256, O=128, H=1, k=1, s=1, p=0, wb=4, ab=4, wbs=1, abs=1, xbar=128, adc=1.5, signed=0),
+    dict(B=128, C=192, O=64, H=1, k=1, s=1, p=0, wb=2, ab=2, wbs=1, abs=1, xbar=64, adc=1.5, signed=0),
+    dict(B=256, C=80, O=64, H=1, k=1, s=1, p=0, wb=3, ab=3, wbs=1, abs=1, xbar=64, adc=1.5, signed=1),
     # sign ADC: sign(ps) at ps = 0 follows the reference's fp32 residues (slice artifacts,
     # summation order), so this case uses power-of-two scales: x_int, w_int exact
     dict(B=2, C=16, O=16, H=16, k=3, s=1, p=1, wb=3, ab=3, wbs=1, abs=1, xbar=128, adc=1, signed=0, sa=0.125,
