@@ -321,6 +321,7 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
   a.napart = act_parts(g);
   a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
+  a.gapart = (has_alpha && la.nalpha > kFinishInReg && tune("WIDE_TAIL", 1)) ? reinterpret_cast<float*>(w + W.gapart) : nullptr;
   j.g = g;
   j.q = la;
   j.tail_blocks = a.nwb + a.nga;
@@ -334,7 +335,10 @@ static int launch_tail(const Carry& j, hipStream_t s) {
 }
 
 static int launch_finish(const Carry& j, hipStream_t s) {
-  hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, j.q, j.a);
+  if (j.a.gapart)
+    hipLaunchKernelGGL(module_bwd_finish_wide_kernel, dim3(cdiv(j.q.nalpha, 1024)), dim3(1024), 0, s, j.q, j.a);
+  else
+    hipLaunchKernelGGL(module_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, j.q, j.a);
   return check_hip("module_bwd_finish");
 }
 
@@ -444,7 +448,14 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
                                           binary_mask, signed_act, c, &nwblk);
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     const int slot = prof_begin(KID_PREP_ACT, g, s);
-    hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, a);
+    ModulePrep aw = a;
+    if (nwblk > 0 && has_alpha && la.nalpha > kFinishInReg && tune("WIDE_PREP", 1)) {  // wide alpha_cim: its max / min in 64 blocks first
+      float* part = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ws) + ws_layout(g).lsq_part);
+      hipLaunchKernelGGL(alpha_minmax_kernel, dim3(64), dim3(256), 0, s, alpha_cim, la.nalpha, part);
+      aw.amm = part;
+      aw.namm = 64;
+    }
+    hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, aw);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("prep_module"));
   }

@@ -420,12 +420,12 @@ inline bool dense_plan(const Geo& g) {
   if (tune("DENSE", 1) == 0) return false;
   if (g.KH != 1 || g.KW != 1 || g.SH != 1 || g.SW != 1 || g.PH != 0 || g.PW != 0 || g.H != 1 || g.W != 1) return false;
   if (g.variant != VAR_LIBRARY || g.mode != ADC_TERNARY || g.NBP != 4 || g.nbw != g.nba || g.nbw > 4) return false;
-  if (g.xbar % 64 != 0 || g.C % 16 != 0 || g.O % 64 != 0 || g.M % 128 != 0) return false;
+  if (g.xbar % 64 != 0 || g.xbar > 128 || g.C % 16 != 0 || g.O % 64 != 0 || g.M % 128 != 0) return false;
   return true;
 }
-// grad_w row chunks: about 512 workgroups over (chunks x tiles x 64-channel groups), 32-row multiples
+// grad_w row chunks: about 512 workgroups over (chunks x tiles x 128-channel groups), 32-row multiples
 inline int dense_chunks(const Geo& g) {
-  const int per = std::max(1, 512 / (g.T * (g.O / 64)));
+  const int per = std::max(1, 512 / (g.T * ((g.O + 127) / 128)));
   return std::max(1, std::min(per, g.M / 256));
 }
 inline int dense_rows_per_chunk(const Geo& g) {
@@ -434,7 +434,7 @@ inline int dense_rows_per_chunk(const Geo& g) {
 }
 
 struct WsLayout {
-  size_t gw_slab, ga_slab, gb_slab, lsq_part, gaq, wpart, bpo, total;
+  size_t gw_slab, ga_slab, gb_slab, lsq_part, gaq, gapart, wpart, bpo, total;
   int rows, nchunks, nchunks_bwd;
 };
 
@@ -455,6 +455,7 @@ inline WsLayout ws_layout(const Geo& g) {
   // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
   // a [B, P, O] staging copy of out / grad_out for the general kernels
   W.gaq = o; o = align256(o + sizeof(float) * (size_t)g.T * g.nbw * g.nba * g.O);
+  W.gapart = o; o = align256(o + sizeof(float) * 4 * (size_t)cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64));
   W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
   W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
   W.total = o;

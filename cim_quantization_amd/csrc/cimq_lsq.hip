@@ -37,6 +37,8 @@ struct ModulePrep {
   float* scal;  // [0] sa, [1] sw, [2] alpha scale, [3] max(alpha_cim), [4] min(alpha_cim)
   int nact_blocks;
   int nwf, nwg, nwt, nwc, npp;  // items of the weight-side roles
+  const float* amm;             // wide alpha_cim: [namm][2] per-block (max, min) of alpha_minmax_kernel
+  int namm;                     // 0: every weight block reduces alpha_cim itself
 };
 
 // the weight side of the prologue: block wb of nwblk (quantised weight operands, alpha_cim's
@@ -55,7 +57,12 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
   if (q.nbits_alpha > 0) {  // lsq.py:566-571
     mx = -INFINITY;
     mn = INFINITY;
-    if (inreg) {
+    if (a.namm > 0) {
+      for (int t = threadIdx.x; t < a.namm; t += blockDim.x) {
+        mx = nan_max(mx, a.amm[2 * t]);
+        mn = nan_min(mn, a.amm[2 * t + 1]);
+      }
+    } else if (inreg) {
 #pragma unroll
       for (int u = 0; u < AP; ++u) {
         const int e = threadIdx.x + u * (int)blockDim.x;
@@ -89,7 +96,15 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
     bool lit = false;
     if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
       lit = !scales_ok(sw, sa);
-      if (as.a && inreg) {
+      if (as.a && a.namm > 0) {
+        // alpha_q is monotone in alpha_cim for a positive finite scale (and 0 / NaN / inf for
+        // every entry otherwise), so its extremes decide: the entries at max and min
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float v = clamp_nan(round_pass_value((u ? mn : mx) / as.scale), 1.f, as.qp_al) * as.scale;
+          lit = lit || !(v > 0.f && isfinite(v));
+        }
+      } else if (as.a && inreg) {
 #pragma unroll
         for (int u = 0; u < AP; ++u) {
           if ((int)threadIdx.x + u * (int)blockDim.x < q.nalpha) {  // as ASrc::get on the loaded value
@@ -184,7 +199,7 @@ __global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q,
   __shared__ float red[1024];
   const int b = (int)blockIdx.x;
   if (b < a.nwb) gw_lsq_role(g, q, a, b, red);
-  else galpha_role(g, a, b - a.nwb, red);
+  else galpha_role(g, q, a, b - a.nwb, red);
 }
 
 // One block: the epilogue's last step after the kernel boundary (which orders the partials
@@ -194,6 +209,29 @@ __global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q,
 __global__ __launch_bounds__(1024) void module_bwd_finish_kernel(LsqArgs q, ModuleTail a) {
   __shared__ __attribute__((aligned(16))) float red[16 * 8];
   module_finish_block(q, a, red);
+}
+
+__global__ __launch_bounds__(1024) void module_bwd_finish_wide_kernel(LsqArgs q, ModuleTail a) {
+  __shared__ __attribute__((aligned(16))) float red[16 * 8];
+  module_finish_wide_block(q, a, red);
+}
+
+// max / min of a wide alpha_cim (> kFinishInReg elements) per block, for the prologue's weight
+// blocks to combine (module_prep_weights) instead of each re-reading all of alpha_cim
+__global__ __launch_bounds__(256) void alpha_minmax_kernel(const float* __restrict__ alpha_cim, int n,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4 * 16];
+  float mx = -INFINITY, mn = INFINITY;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const float v = alpha_cim[e];
+    mx = nan_max(mx, v);
+    mn = nan_min(mn, v);
+  }
+  const float2 r = block_max_min(mx, mn, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = r.x;
+    part[2 * blockIdx.x + 1] = r.y;
+  }
 }
 
 // layout changes for the general (non-fast-path) kernels in module mode

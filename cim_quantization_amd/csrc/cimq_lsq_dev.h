@@ -84,9 +84,14 @@ struct ModuleTail {
   float* grad_alpha_w;
   float* grad_alpha_cim;
   Params pp;
-  float cgrad;  // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
+  float* gapart;  // wide alpha_cim (> kFinishInReg elements): [nga][4] first-sweep partials, else null
+  float cgrad;    // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
   int nchunks, nwb, nga, napart, accum;
 };
+// alpha_cim sizes the one-block epilogue keeps in registers (module_finish_block); larger ones
+// (the QuantLinear layers: T * nbw * nba * O = 131072 at 1024 -> 1024 w4a4) take the wide path:
+// the first sweep's partials per tail block, then a grid-wide second sweep.
+constexpr int kFinishInReg = 8 * 1024;
 
 // grad_w slab sum -> G = d loss / d w_q, then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
 //   grad_weight = mask * (G * sw) / sw; per block the partial sums of G * rp (MulBackward,
@@ -133,20 +138,46 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
   }
 }
 
-__device__ inline void galpha_role(const Geo& g, const ModuleTail& a, int blk, float* red) {
+__device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const int nkj = g.nbw * g.nba;
   const size_t nout = (size_t)g.T * nkj * g.Opad;
   const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
   const float s = reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  if ((threadIdx.x >> 6) == 0 && idx < nout) {
+  if ((threadIdx.x >> 6) != 0) return;
+  float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (idx < nout) {
     const int o = (int)(idx % g.Opad);
     const size_t qq = idx / g.Opad;  // (i, k, j)
     if (o < g.O) {
       const int kj = (int)(qq % nkj);
       const int i = (int)(qq / nkj);
       const int k = kj / g.nba, j = kj - k * g.nba;
-      a.gaq[(((size_t)i * g.nbw + k) * g.nba + j) * g.O + o] = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
+      const size_t e = (((size_t)i * g.nbw + k) * g.nba + j) * g.O + o;
+      const float G = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
+      a.gaq[e] = G;
+      if (a.gapart) {  // alpha_cim_bwd_block's first sweep, this element
+        const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
+        const float qp_al = (float)((1 << q.nbits_alpha) - 1);
+        const float v = a.alpha_cim[e];
+        const float t = v / scale;
+        const float rp = round_pass_value(t);
+        const float c = clamp_nan(rp, 1.f, qp_al);
+        const bool pass = (rp >= 1.f) && (rp <= qp_al);
+        const float gt = pass ? G * scale : 0.f;
+        part = make_float4(G * c, -gt * (t / scale), ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f,
+                           ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f);
+      }
     }
+  }
+  if (a.gapart) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      part.x += __shfl_xor(part.x, off);
+      part.y += __shfl_xor(part.y, off);
+      part.z += __shfl_xor(part.z, off);
+      part.w += __shfl_xor(part.w, off);
+    }
+    if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = part;
   }
 }
 
@@ -313,6 +344,41 @@ __device__ inline void module_finish_block(const LsqArgs& q, const ModuleTail& a
     a.grad_alpha_w[0] = a.accum ? a.grad_alpha_w[0] + gw : gw;
     a.grad_alpha_act[0] = a.accum ? a.grad_alpha_act[0] + ga : ga;
   }
+}
+
+// The wide epilogue's last step (module_bwd_finish_wide_kernel, a.gapart set): every block sums
+// the tail blocks' first-sweep partials in the same order, then runs the second sweep of
+// alpha_cim_bwd_block over its 1024-element slice; block 0 also finishes the step sizes.
+__device__ inline void module_finish_wide_block(const LsqArgs& q, const ModuleTail& a, float* red) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = threadIdx.x; t < a.nga; t += blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(a.gapart)[t];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  const float4 r = block_sum4(acc, red);
+  const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
+  const float qp_al = (float)((1 << q.nbits_alpha) - 1);
+  const float N = (float)((1 << q.nbits_alpha) - 2);
+  const float gdiff = (r.x + r.y) / N;  // d loss / d scale, then DivBackward of (max - min) / N
+  const float pmax = gdiff / r.z, pmin = -gdiff / r.w;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < q.nalpha) {
+    const float v = a.alpha_cim[e];
+    const float t = v / scale;
+    const float rp = round_pass_value(t);
+    const bool pass = (rp >= 1.f) && (rp <= qp_al);
+    const float gt = pass ? a.gaq[e] * scale : 0.f;
+    const bool ismin = (mn != mn) ? (v != v) : (v == mn);
+    const bool ismax = (mx != mx) ? (v != v) : (v == mx);
+    float rr = gt / scale;
+    rr = rr + (ismin ? pmin : 0.f);
+    rr = rr + (ismax ? pmax : 0.f);
+    a.grad_alpha_cim[e] = a.accum ? a.grad_alpha_cim[e] + rr : rr;
+  }
+  if (blockIdx.x == 0) lsq_finish_block(q, a, red);
 }
 
 // A previous layer's finish (module_finish_block) run by block 0 of this layer's v7 grad_x

@@ -9,9 +9,10 @@
 //   grad_w   gw[c, o]  = sa/nbw * sum_j sum_m xhat_j[m, c] * g[m, o] * D_ij[m, o]
 //            (both v_mfma_f32_16x16x32_bf16, the fp32 operand split hi/mid/lo: lsq.py:336-386)
 //
-// The forward leaves per (tile i, row m, channel o) a uint2 of three 16-bit planes -- STE pass,
-// ADC code != 0, code < 0, bit k*nba + j -- instead of the fp16 partial sums (lsq.py:169-192);
-// the backward kernels decode E / D / the ADC code from them.  grad_w and grad_alpha leave
+// The forward leaves per (tile i, row m, channel o) a uint2 instead of the fp16 partial sums
+// (lsq.py:169-192): .x the ADC codes as 2-bit two's-complement fields (bits 2kj, 2kj+1 of slice
+// pair kj = k*nba + j: 00 = 0, 01 = +1, 11 = -1), .y the STE pass bits (bit kj); the backward
+// kernels decode E / D from the pass bits and grad_alpha's code * g from the fields.  grad_w and grad_alpha leave
 // per-chunk slabs in the layout the module epilogue reduces (module_bwd_tail_kernel).
 // Own translation unit of libcimq.so.
 #define CIMQ_TU_DENSE
@@ -27,37 +28,64 @@ __device__ inline uint32_t dmask_j(int j, int nbw, int nba) {
   return m;
 }
 
+// One partial sum's ternary ADC and state bits in one block of instructions: the three compare
+// masks live in SGPRs only between their compare and their use (left to the compiler, the
+// compares of all 16 partial sums of a slice-pair group are hoisted and their masks spill).
+//   acc += hi ? cf : (lo ? -cf : 0);  pass / hi / lo shifted in at bit 0 of sp / shi / slo
+// The subtraction stays compiler code: it is the first read of the MFMA result, so the hazard
+// recognizer pads it (it does not look into inline asm); the asm reads ps only after it.
+__device__ inline void adc_ps(int ps, int4 pv, float cf, float& acc, uint32_t& sp, uint32_t& shi, uint32_t& slo) {
+  const int t = (int)((unsigned)ps - (unsigned)pv.z);
+  uint64_t mh, ml, mp, co;
+  float a;
+  asm("v_cmp_ge_i32_e64 %[mh], %[ps], %[thi]\n\t"
+      "v_cmp_le_i32_e64 %[ml], %[ps], %[tlo]\n\t"
+      "v_cmp_le_u32_e64 %[mp], %[t], %[span]\n\t"
+      "v_cndmask_b32_e64 %[a], 0, %[cf], %[mh]\n\t"
+      "v_cndmask_b32_e64 %[a], %[a], -%[cf], %[ml]\n\t"
+      "v_add_f32_e32 %[acc], %[acc], %[a]\n\t"
+      "v_addc_co_u32_e64 %[sp], %[co], %[sp], %[sp], %[mp]\n\t"
+      "v_addc_co_u32_e64 %[shi], %[co], %[shi], %[shi], %[mh]\n\t"
+      "v_addc_co_u32_e64 %[slo], %[co], %[slo], %[slo], %[ml]"
+      : [mh] "=&s"(mh), [ml] "=&s"(ml), [mp] "=&s"(mp), [co] "=&s"(co), [a] "=&v"(a),
+        [acc] "+v"(acc), [sp] "+v"(sp), [shi] "+v"(shi), [slo] "+v"(slo)
+      : [ps] "v"(ps), [t] "v"(t), [thi] "v"(pv.x), [tlo] "v"(pv.y), [span] "v"(pv.w), [cf] "v"(cf));
+}
+
+// bit b of a 16-bit plane -> bit 2b
+__device__ inline uint32_t spread16(uint32_t x) {
+  x &= 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  return (x | (x << 1)) & 0x55555555u;
+}
+
 // ---------------------------------------------------------------------------------------------
-// forward: block = 64 rows x 64 channels, wave w = rows 16w..16w+15 x four 16-channel blocks
+// forward: block = 64 rows x 64 channels, wave w = rows 16w..16w+15 x four 16-channel blocks (in turn)
 // ---------------------------------------------------------------------------------------------
-template <int NBW, int NBA, int KS>
-__global__ __launch_bounds__(256) void dense_fwd_kernel(Geo g, const uint8_t* __restrict__ xcf,
-                                                        const v4i* __restrict__ wfrag, Params pp,
-                                                        const float* __restrict__ sw_p, const float* __restrict__ sa_p,
-                                                        float* __restrict__ out, uint2* __restrict__ st) {
+template <int NBW, int NBA, int KS, bool LIT>
+__device__ inline void dense_fwd_body(const Geo& g, const uint8_t* __restrict__ xcf, const v4i* __restrict__ wfrag,
+                                      const Params& pp, float sw, float sa, float* __restrict__ out,
+                                      uint2* __restrict__ st, int4* prm, float* cfl, float4* accs, int m0,
+                                      int og) {
   constexpr int NKJ = NBW * NBA;
-  __shared__ int4 prm[NKJ * 64];  // this tile's ADC / STE thresholds, [j][k][64 channels]
-  __shared__ float cfl[NKJ * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int m0 = blockIdx.x * 64, og = blockIdx.y;
-  const float sw = *sw_p, sa = *sa_p;
-  const bool literal = pp.flags[0] != 0;
   const int mrow = m0 + wave * 16 + r16;  // this lane's A row
-  float acc[4][4];
-#pragma unroll
-  for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
+  // out accumulators of the four channel blocks in LDS ([wave][ob][lane]); one block's in registers
+  float4* acc_l = accs + wave * 4 * 64 + lane;
   for (int i = 0; i < g.T; ++i) {
-    __syncthreads();
-    for (int t = threadIdx.x; t < NKJ * 64; t += 256) {
-      const int col = t & 63, jk = t >> 6, j = jk / NBW, k = jk - j * NBW;
-      const int pi = pidx(g, i, j, k, og * 64 + col);
-      prm[t] = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
-      cfl[t] = pp.coef[pi];
+    if (!LIT) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < NKJ * 64; t += 256) {
+        const int col = t & 63, jk = t >> 6, j = jk / NBW, k = jk - j * NBW;
+        const int pi = pidx(g, i, j, k, og * 64 + col);
+        prm[t] = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
+        cfl[t] = pp.coef[pi];
+      }
+      __syncthreads();
     }
-    __syncthreads();
     // A operands: slice j of the 16 channels c0 .. c0+15 of row mrow, c0 = i*xbar + 64ks + 16 g4
     // (4-byte slice words, byte j = slice j: a 4x4 byte transpose per 4 channels)
     v4i xs[NBA][KS];
@@ -84,16 +112,22 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(Geo g, const uint8_t* __
         for (int j = 0; j < NBA; ++j) xs[j][ks][q] = (int)P[j];
       }
     }
-    uint32_t sp[4][4], sz[4][4], sn[4][4];  // the three 16-bit state planes of (channel block, row)
+    // one 16-channel block at a time: its three 16-bit state planes live only across the slice pairs
+#pragma unroll 1
+    for (int ob = 0; ob < 4; ++ob) {
+      float acc[4];
+      if (i == 0) {
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+      } else {
+        const float4 a4 = acc_l[ob * 64];
+        acc[0] = a4.x; acc[1] = a4.y; acc[2] = a4.z; acc[3] = a4.w;
+      }
+      uint32_t sp[4], sz[4], sn[4];
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
+      for (int r = 0; r < 4; ++r) sp[r] = sz[r] = sn[r] = 0u;
+      // slice pairs in descending kj = k*nba + j order: shifting each bit in from the bottom leaves it at bit kj
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sp[ob][r] = sz[ob][r] = sn[ob][r] = 0u;
-    // slice pairs in descending kj = k*nba + j order: shifting each bit in from the bottom leaves it at bit kj
-#pragma unroll
-    for (int k = NBW - 1; k >= 0; --k) {
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
+      for (int k = NBW - 1; k >= 0; --k) {
         v4i wk[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) wk[ks] = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * 4 + ob) * 64 + lane];
@@ -106,20 +140,12 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(Geo g, const uint8_t* __
         }
 #pragma unroll
         for (int j = NBA - 1; j >= 0; --j) {
-          const int pcol = (j * NBW + k) * 64 + ob * 16 + r16;
-          const int4 pv = prm[pcol];
-          const float cf = cfl[pcol];
-          if (!literal) {
+          if (!LIT) {
+            const int pcol = (j * NBW + k) * 64 + ob * 16 + r16;
+            const int4 pv = prm[pcol];
+            const float cf = cfl[pcol];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
-              const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
-              const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(ps[j][r] - pv.z) <= (unsigned)pv.w);
-              acc[ob][r] += adc3(cf, mhi, mlo);
-              sp[ob][r] = shin(sp[ob][r], mps);
-              sz[ob][r] = shin(sz[ob][r], mhi | mlo);
-              sn[ob][r] = shin(sn[ob][r], mlo);
-            }
+            for (int r = 0; r < 4; ++r) adc_ps(ps[j][r], pv, cf, acc[r], sp[r], sz[r], sn[r]);
           } else {
             // degenerate alpha / scales: the literal ADC per partial sum (as cim_fwd_v3_kernel)
             const int o = og * 64 + ob * 16 + r16;
@@ -127,246 +153,328 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(Geo g, const uint8_t* __
             const float mk = pp.ckj[k * NBA + j];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              acc[ob][r] += adc_literal_sum(ps[j], g.mode, sw, sa, al, g.qn, g.qp, mk, r);
+              acc[r] += adc_literal_sum(ps[j], g.mode, sw, sa, al, g.qn, g.qp, mk, r);
               const bool pass = ste_literal(ps[j][r], g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f;
               const float code = code_literal(ps[j][r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo);
-              sp[ob][r] = (sp[ob][r] << 1) | (pass ? 1u : 0u);
-              sz[ob][r] = (sz[ob][r] << 1) | (code != 0.f ? 1u : 0u);
-              sn[ob][r] = (sn[ob][r] << 1) | (code < 0.f ? 1u : 0u);
+              sp[r] = (sp[r] << 1) | (pass ? 1u : 0u);
+              sz[r] = (sz[r] << 1) | (code > 0.f ? 1u : 0u);
+              sn[r] = (sn[r] << 1) | (code < 0.f ? 1u : 0u);
             }
           }
         }
       }
-    }
-    // state of rows m0 + 16w + 4g4 + r (MFMA output rows), channel og*64 + 16ob + r16
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
+      // state of rows m0 + 16w + 4g4 + r (MFMA output rows), channel og*64 + 16ob + r16
       const int o = og * 64 + ob * 16 + r16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const size_t m = (size_t)m0 + wave * 16 + 4 * g4 + r;
-        st[((size_t)i * g.M + m) * g.O + o] = make_uint2((sp[ob][r] & 0xFFFFu) | (sz[ob][r] << 16), sn[ob][r] & 0xFFFFu);
+        // code fields: lo -> 11, hi -> 01 (lo wins, as the ADC's second select)
+        const uint32_t code = spread16(sz[r] | sn[r]) | (spread16(sn[r]) << 1);
+        st[((size_t)i * g.M + m) * g.O + o] = make_uint2(code, sp[r] & 0xFFFFu);
+      }
+      if (i + 1 < g.T) {
+        acc_l[ob * 64] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[((size_t)m0 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[r];
       }
     }
   }
-#pragma unroll
-  for (int ob = 0; ob < 4; ++ob) {
-    const int o = og * 64 + ob * 16 + r16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) out[((size_t)m0 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[ob][r];
-  }
+}
+
+// The threshold path: one 64 x 64 tile per block.  Exits at once when the prologue set the
+// literal-ADC flag (dense_fwd_lit_kernel then does the work).
+template <int NBW, int NBA, int KS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void dense_fwd_kernel(
+    Geo g, const uint8_t* __restrict__ xcf, const v4i* __restrict__ wfrag, Params pp, const float* __restrict__ sw_p,
+    const float* __restrict__ sa_p, float* __restrict__ out, uint2* __restrict__ st) {
+  __shared__ int4 prm[NBW * NBA * 64];  // this tile's ADC / STE thresholds, [j][k][64 channels]
+  __shared__ float cfl[NBW * NBA * 64];
+  __shared__ float4 accs[4 * 4 * 64];
+  if (__builtin_amdgcn_readfirstlane(pp.flags[0]) != 0) return;
+  dense_fwd_body<NBW, NBA, KS, false>(g, xcf, wfrag, pp, 0.f, 0.f, out, st, prm, cfl, accs, blockIdx.x * 64,
+                                      blockIdx.y);
+}
+
+// Degenerate alpha_q / scales (flag set): the literal ADC per partial sum, a few blocks looping
+// over the tiles (its out-of-line calls kept out of the threshold kernel's register budget).
+template <int NBW, int NBA, int KS>
+__global__ __launch_bounds__(256) void dense_fwd_lit_kernel(Geo g, const uint8_t* __restrict__ xcf,
+                                                            const v4i* __restrict__ wfrag, Params pp,
+                                                            const float* __restrict__ sw_p,
+                                                            const float* __restrict__ sa_p, float* __restrict__ out,
+                                                            uint2* __restrict__ st) {
+  __shared__ float4 accs[4 * 4 * 64];
+  if (__builtin_amdgcn_readfirstlane(pp.flags[0]) == 0) return;
+  const float sw = *sw_p, sa = *sa_p;
+  const int nm = g.M / 64, ntile = nm * (g.O / 64);
+  for (int t = blockIdx.x; t < ntile; t += gridDim.x)
+    dense_fwd_body<NBW, NBA, KS, true>(g, xcf, wfrag, pp, sw, sa, out, st, nullptr, nullptr, accs, (t % nm) * 64, t / nm);
 }
 
 // ---------------------------------------------------------------------------------------------
-// grad_x: block = 128 rows x one crossbar tile's channels (FBT blocks of 16); wave w = rows
-// 32w..32w+31 (two MFMA row blocks).  A = G_i (rows m, built from the state planes and g in
-// registers), B = the int8 ctx weight slices as bf16 (wgx_item: columns c, kappa = (k, o) order).
+// grad_x: block = 128 rows x one crossbar tile (<= 8 blocks of 16 channels), 8 waves.  Per K-step
+// of 32 kappa = (k, o) the whole block builds the A operand G_i[m, kappa] = g[m, o] * E_ik[m, o]
+// (hi / mid / lo bf16) into LDS -- wave w the rows 16w..16w+15, each lane one MFMA fragment -- and
+// wave w then multiplies rows 32(w&3)..+31 by the channel blocks 4(w>>2)..+3, the B fragments (the
+// int8 ctx weight slices as bf16, wgx_item layout) read from global one step ahead.  K-steps run
+// o-pair major, slice k minor, so a lane loads each of its state words and g values once.
 // ---------------------------------------------------------------------------------------------
 template <int NBW, int NBA>
-__global__ __launch_bounds__(256) void dense_gx_kernel(Geo g, const uint2* __restrict__ st, const v4i* __restrict__ wgx,
+__global__ __launch_bounds__(512) void dense_gx_kernel(Geo g, const uint2* __restrict__ st, const v4i* __restrict__ wgx,
                                                        Params pp, const float* __restrict__ sw_p,
                                                        const float* __restrict__ gout, float* __restrict__ gx) {
   constexpr int NKJ = NBW * NBA;
-  constexpr int FBX = 8;  // dense plan: xbar <= 128
+  __shared__ v4i Gs[2 * 3 * 8 * 64];  // [buffer][hi/mid/lo][16-row block][lane]
   __shared__ float cel[NKJ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int m0 = blockIdx.x * 128 + wave * 32, i = blockIdx.y;
-  for (int t = threadIdx.x; t < NKJ; t += 256) cel[t] = pp.ckj[NKJ + t];
+  const int m0 = blockIdx.x * 128, i = blockIdx.y;
+  const int rg = wave & 3, chh = wave >> 2;
+  for (int t = threadIdx.x; t < NKJ; t += 512) cel[t] = pp.ckj[NKJ + t];
   __syncthreads();
   bool std_mask;  // cE_kj = 2^(bsw*k) for every j: E_k = 2^(bsw*k) * popcount(pass bits of slice k)
   {
     const int kl = lane < NKJ ? lane / NBA : 0;
     std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cel[lane < NKJ ? lane : 0] != ldexpf(1.f, g.bsw * kl)) == 0ull;
   }
-  v4f acc[2][FBX];
+  // builder: row m0 + 16 wave + r16, kappa channels 32p + 4g4 + e (e < 4) and 32p + 16 + 4g4 + e
+  const size_t mb = (size_t)m0 + 16 * wave + r16;
+  const uint2* strow = st + ((size_t)i * g.M + mb) * g.O + 4 * g4;
+  const float* grow = gout + mb * g.O + 4 * g4;
+  uint32_t pw[8];
+  float gv[8];
+  auto load_p = [&](int p) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(strow + 32 * p);
+    const uint4 a0 = s4[0], a1 = s4[1], b0 = s4[8], b1 = s4[9];
+    pw[0] = a0.y; pw[1] = a0.w; pw[2] = a1.y; pw[3] = a1.w;  // pass bits
+    pw[4] = b0.y; pw[5] = b0.w; pw[6] = b1.y; pw[7] = b1.w;
+    const float4 ga = *reinterpret_cast<const float4*>(grow + 32 * p);
+    const float4 gb = *reinterpret_cast<const float4*>(grow + 32 * p + 16);
+    gv[0] = ga.x; gv[1] = ga.y; gv[2] = ga.z; gv[3] = ga.w;
+    gv[4] = gb.x; gv[5] = gb.y; gv[6] = gb.z; gv[7] = gb.w;
+  };
+  auto build = [&](int k, int buf) {
+    float Gv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float E;
+      if (std_mask) {
+        E = ldexpf((float)__popc(pw[e] & dmask_k(k, NBA)), g.bsw * k);
+      } else {
+        E = 0.f;
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) E += ((pw[e] >> (k * NBA + j)) & 1u) ? cel[k * NBA + j] : 0.f;
+      }
+      Gv[e] = gv[e] * E;
+    }
+    v8bf h, md, lo;
+    split3x8(Gv, h, md, lo);
+    v4i* dst = Gs + (buf * 3 * 8 + wave) * 64 + lane;
+    dst[0] = as_v4i(h);
+    dst[8 * 64] = as_v4i(md);
+    dst[16 * 64] = as_v4i(lo);
+  };
+  const int hp = g.OB16 / 2;  // o-pairs (O % 64 == 0)
+  const int nsteps = NBW * hp;
+  auto step_s = [&](int t) { return (t % NBW) * hp + t / NBW; };
+  const int nf = min(4, g.FBT - 4 * chh);  // this wave's channel blocks (0 when the tile has 4)
+  const v4i* wt = wgx + ((size_t)i * g.FBT + 4 * chh) * g.NKS * 64 + lane;
+  v4i bc[4], bn[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) bc[f] = f < nf ? wt[((size_t)f * g.NKS + step_s(0)) * 64] : v4i{0, 0, 0, 0};
+  load_p(0);
+  build(0, 0);
+  __syncthreads();
+  v4f acc[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int fb = 0; fb < FBX; ++fb) acc[h][fb] = v4f{0.f, 0.f, 0.f, 0.f};
-  const v4i* wt = wgx + (size_t)i * g.FBT * g.NKS * 64 + lane;
-  for (int s = 0; s < g.NKS; ++s) {
-    v8bf Gh[2], Gm[2], Gl[2];
+    for (int f = 0; f < 4; ++f) acc[h][f] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < nsteps; ++t) {
+    const int tn = t + 1;
+    if (tn < nsteps) {
+      const int sn = step_s(tn);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // row block h: rows m0 + 16h + r16
-      const size_t m = (size_t)m0 + 16 * h + r16;
-      float Gv[8];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {  // kappa block kb = 2s + hh: (k, o-block), 4 channels o0 .. o0+3
-        const int kb = 2 * s + hh;
-        if (kb < g.NBLK) {
-          const int k = kb / g.OB16, o0 = (kb - k * g.OB16) * 16 + 4 * g4;
-          const uint4* sp4 = reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + o0);
-          const uint4 a = sp4[0], b = sp4[1];
-          const float4 gg = *reinterpret_cast<const float4*>(gout + m * g.O + o0);
-          const uint32_t pw[4] = {a.x, a.z, b.x, b.z};  // pass planes (low 16 bits)
-          const float gv[4] = {gg.x, gg.y, gg.z, gg.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float E;
-            if (std_mask) {
-              E = ldexpf((float)__popc(pw[e] & dmask_k(k, NBA)), g.bsw * k);
-            } else {
-              E = 0.f;
-#pragma unroll
-              for (int j = 0; j < NBA; ++j) E += ((pw[e] >> (k * NBA + j)) & 1u) ? cel[k * NBA + j] : 0.f;
-            }
-            Gv[4 * hh + e] = gv[e] * E;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) Gv[4 * hh + e] = 0.f;
-        }
-      }
-      split3x8(Gv, Gh[h], Gm[h], Gl[h]);
+      for (int f = 0; f < 4; ++f) bn[f] = f < nf ? wt[((size_t)f * g.NKS + sn) * 64] : v4i{0, 0, 0, 0};
+      if (tn % NBW == 0) load_p(tn / NBW);
     }
-#pragma unroll
-    for (int fb = 0; fb < FBX; ++fb) {
-      if (fb >= g.FBT) break;
-      const v8bf bw = as_v8bf(wt[((size_t)fb * g.NKS + s) * 64]);
+    if (nf > 0) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        acc[h][fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Gh[h], bw, acc[h][fb], 0, 0, 0);
-        acc[h][fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Gm[h], bw, acc[h][fb], 0, 0, 0);
-        acc[h][fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Gl[h], bw, acc[h][fb], 0, 0, 0);
+        const v4i* src = Gs + ((t & 1) * 3 * 8 + 2 * rg + h) * 64 + lane;
+        const v8bf ah = as_v8bf(src[0]), am = as_v8bf(src[8 * 64]), al = as_v8bf(src[16 * 64]);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const v8bf bw = as_v8bf(bc[f]);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, acc[h][f], 0, 0, 0);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, acc[h][f], 0, 0, 0);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, acc[h][f], 0, 0, 0);
+        }
       }
     }
+    if (tn < nsteps) build(tn % NBW, tn & 1);
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < 4; ++f) bc[f] = bn[f];
   }
   const float scale = *sw_p / (float)NBA;
 #pragma unroll
-  for (int fb = 0; fb < FBX; ++fb) {
-    if (fb >= g.FBT) break;
-    const int c = i * g.xbar + fb * 16 + r16;
-    if (c < g.C && fb * 16 < g.xbar) {
+  for (int f = 0; f < 4; ++f) {
+    if (f >= nf) break;
+    const int c = i * g.xbar + (4 * chh + f) * 16 + r16;
+    if (c < g.C) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gx[((size_t)m0 + 16 * h + 4 * g4 + r) * g.C + c] = acc[h][fb][r] * scale;
+        for (int r = 0; r < 4; ++r) gx[((size_t)m0 + 32 * rg + 16 * h + 4 * g4 + r) * g.C + c] = acc[h][f][r] * scale;
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// grad_w + grad_alpha partials: block = (row chunk, tile i, 64 channels o); wave w = channel block
-// 4 blockIdx.z + w.  K-step = 32 rows: A = xhat_j[m, c] of the tile's channels (built once per
-// step by the whole block into LDS), B = g * D_j (registers).  grad_alpha: sum of code * g.
+// grad_w + grad_alpha partials: block = (row chunk, tile i, 128 channels o), 8 waves; wave w =
+// channel block 8 blockIdx.z + w.  K-step = 32 rows: A = xhat_j[m, c] of the tile's channels,
+// built by the whole block into LDS one step ahead (double buffer, its words loaded two steps
+// ahead), B = g * D_j (registers).  grad_alpha: sum over the rows of code * g per slice pair.
 // ---------------------------------------------------------------------------------------------
 template <int NBW, int NBA>
-__global__ __launch_bounds__(256) void dense_gw_kernel(Geo g, int rows_per_chunk, const uint2* __restrict__ st,
+__global__ __launch_bounds__(512) void dense_gw_kernel(Geo g, int rows_per_chunk, const uint2* __restrict__ st,
                                                        const uint8_t* __restrict__ xcb, Params pp,
                                                        const float* __restrict__ gout, float* __restrict__ gw_slab,
                                                        float* __restrict__ ga_slab) {
   constexpr int NKJ = NBW * NBA;
   constexpr int FBX = 8;
-  __shared__ v4i As[FBX * NBA * 64];  // [fb][j][64 lanes]: 8 bf16 of rows c, contraction 8 rows m
+  __shared__ v4i As[2 * FBX * NBA * 64];  // [buffer][fb][j][64 lanes]: 8 bf16 of rows c, contraction 8 rows m
   __shared__ float cdl[NKJ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int chunk = blockIdx.x, i = blockIdx.y;
-  const int o = (blockIdx.z * 4 + wave) * 16 + r16;  // this lane's B column
-  for (int t = threadIdx.x; t < NKJ; t += 256) cdl[t] = pp.ckj[2 * NKJ + t];
+  const int ob = blockIdx.z * 8 + wave;
+  const bool oact = ob * 16 < g.O;     // waves past the last channel block only build A
+  const int o = min(ob * 16 + r16, g.O - 1);  // this lane's B column
+  for (int t = threadIdx.x; t < NKJ; t += 512) cdl[t] = pp.ckj[2 * NKJ + t];
   __syncthreads();
   bool std_mask;  // cD_kj = 2^(bsa*j) for every k: D_j = 2^(bsa*j) * popcount(pass bits of slice j)
   {
     const int kl = lane < NKJ ? lane / NBA : 0, jl = lane < NKJ ? lane - kl * NBA : 0;
     std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cdl[lane < NKJ ? lane : 0] != ldexpf(1.f, g.bsa * jl)) == 0ull;
   }
+  // A builder: item (fb, l) = thread, rows c = i*xbar + 16fb + (l&15), rows m = ms + 8(l>>4) + e
+  const int ifb = threadIdx.x >> 6;
+  const bool ibld = ifb < g.FBT;
+  const int ic = i * g.xbar + ifb * 16 + r16;
+  const bool icok = ibld && ic < g.C && ifb * 16 < g.xbar;
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(xcb) + (icok ? ic : 0);
+  const int mlo = chunk * rows_per_chunk, mhi = min(g.M, mlo + rows_per_chunk);
+  uint32_t aw[8];
+  auto load_a = [&](int ms) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = ms + 8 * g4 + e;
+      aw[e] = (icok && m < mhi) ? xw[(size_t)m * g.C] : 0u;
+    }
+  };
+  auto build_a = [&](int buf) {
+    if (!ibld) return;
+#pragma unroll
+    for (int j = 0; j < NBA; ++j) {
+      uint32_t pk[4];
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) {
+        const float f0 = (float)(int8_t)((aw[2 * e2] >> (8 * j)) & 0xFFu);
+        const float f1 = (float)(int8_t)((aw[2 * e2 + 1] >> (8 * j)) & 0xFFu);
+        pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);  // exact bf16
+      }
+      As[((buf * FBX + ifb) * NBA + j) * 64 + lane] = v4i{(int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]};
+    }
+  };
   v4f acc[FBX];
 #pragma unroll
   for (int fb = 0; fb < FBX; ++fb) acc[fb] = v4f{0.f, 0.f, 0.f, 0.f};
   float qa[NKJ];
 #pragma unroll
   for (int kj = 0; kj < NKJ; ++kj) qa[kj] = 0.f;
-  const int mlo = chunk * rows_per_chunk, mhi = min(g.M, mlo + rows_per_chunk);
+  load_a(mlo);
+  build_a(0);
+  if (mlo + 32 < mhi) load_a(mlo + 32);
+  __syncthreads();
+  int cur = 0;
   for (int ms = mlo; ms < mhi; ms += 32) {
-    __syncthreads();
-    // A fragments of the step: item (fb, l) = rows c = i*xbar + 16fb + (l&15), rows m = ms + 8(l>>4) + e
-    for (int it = threadIdx.x; it < g.FBT * 64; it += 256) {
-      const int fb = it >> 6, l = it & 63;
-      const int c = i * g.xbar + fb * 16 + (l & 15);
-      uint32_t w[8];
+    if (oact) {
+      // B: rows m = ms + 8 g4 + e of channel o
+      float gv[8];
+      uint2 sv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int m = ms + 8 * (l >> 4) + e;
-        w[e] = (c < g.C && fb * 16 < g.xbar && m < mhi) ? reinterpret_cast<const uint32_t*>(xcb)[(size_t)m * g.C + c] : 0u;
+        const int m = ms + 8 * g4 + e;
+        const bool ok = m < mhi;
+        gv[e] = ok ? gout[(size_t)m * g.O + o] : 0.f;
+        sv[e] = ok ? st[((size_t)i * g.M + m) * g.O + o] : make_uint2(0u, 0u);
+      }
+      // grad_alpha partials (lsq.py:321-333): code * g, code the 2-bit field of slice pair kj
+#pragma unroll
+      for (int kj = 0; kj < NKJ; ++kj) {
+        float q = qa[kj];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // the field sign-extended by shifts (the sbfe builtin's result is converted as unsigned)
+          const int code = (int)(sv[e].x << (30 - 2 * kj)) >> 30;
+          q = __builtin_fmaf((float)code, gv[e], q);
+        }
+        qa[kj] = q;
       }
 #pragma unroll
       for (int j = 0; j < NBA; ++j) {
-        uint32_t pk[4];
+        float d[8];
 #pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          const float f0 = (float)(int8_t)((w[2 * e2] >> (8 * j)) & 0xFFu);
-          const float f1 = (float)(int8_t)((w[2 * e2 + 1] >> (8 * j)) & 0xFFu);
-          pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);  // exact bf16
+        for (int e = 0; e < 8; ++e) {
+          float D;
+          if (std_mask) {
+            D = ldexpf((float)__popc(sv[e].y & dmask_j(j, NBW, NBA)), g.bsa * j);
+          } else {
+            D = 0.f;
+#pragma unroll
+            for (int k = 0; k < NBW; ++k) D += ((sv[e].y >> (k * NBA + j)) & 1u) ? cdl[k * NBA + j] : 0.f;
+          }
+          d[e] = gv[e] * D;
         }
-        As[(fb * NBA + j) * 64 + l] = v4i{(int)pk[0], (int)pk[1], (int)pk[2], (int)pk[3]};
+        v8bf bh, bm, bl;
+        split3x8(d, bh, bm, bl);
+#pragma unroll
+        for (int fb = 0; fb < FBX; ++fb) {
+          if (fb >= g.FBT) break;
+          const v8bf a = as_v8bf(As[((cur * FBX + fb) * NBA + j) * 64 + lane]);
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
+        }
       }
+    }
+    if (ms + 32 < mhi) {
+      build_a(cur ^ 1);
+      if (ms + 64 < mhi) load_a(ms + 64);
     }
     __syncthreads();
-    // B: rows m = ms + 8 g4 + e of channel o
-    float gv[8];
-    uint2 sv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int m = ms + 8 * g4 + e;
-      const bool ok = m < mhi;
-      gv[e] = ok ? gout[(size_t)m * g.O + o] : 0.f;
-      sv[e] = ok ? st[((size_t)i * g.M + m) * g.O + o] : make_uint2(0u, 0u);
-    }
-    // grad_alpha partials (lsq.py:321-333): code * g, code from the nz / neg planes
-#pragma unroll
-    for (int kj = 0; kj < NKJ; ++kj) {
-      float q = qa[kj];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t nz = (sv[e].x >> (16 + kj)) & 1u, ng = (sv[e].y >> kj) & 1u;
-        const float code = nz ? (ng ? -1.f : 1.f) : 0.f;
-        q = __builtin_fmaf(code, gv[e], q);
-      }
-      qa[kj] = q;
-    }
-#pragma unroll
-    for (int j = 0; j < NBA; ++j) {
-      float d[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float D;
-        if (std_mask) {
-          D = ldexpf((float)__popc(sv[e].x & dmask_j(j, NBW, NBA)), g.bsa * j);
-        } else {
-          D = 0.f;
-#pragma unroll
-          for (int k = 0; k < NBW; ++k) D += ((sv[e].x >> (k * NBA + j)) & 1u) ? cdl[k * NBA + j] : 0.f;
-        }
-        d[e] = gv[e] * D;
-      }
-      v8bf bh, bm, bl;
-      split3x8(d, bh, bm, bl);
-#pragma unroll
-      for (int fb = 0; fb < FBX; ++fb) {
-        if (fb >= g.FBT) break;
-        const v8bf a = as_v8bf(As[(fb * NBA + j) * 64 + lane]);
-        acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
-        acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
-        acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
-      }
-    }
+    cur ^= 1;
   }
+  if (!oact) return;
   // acc[fb][r]: row c = 16fb + 4g4 + r of the tile, column o
   const int FR = g.FBT * 16;
+  const int oo = ob * 16 + r16;
 #pragma unroll
   for (int fb = 0; fb < FBX; ++fb) {
     if (fb >= g.FBT) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      gw_slab[(((size_t)chunk * g.T + i) * FR + fb * 16 + 4 * g4 + r) * g.Opad + o] = acc[fb][r];
+      gw_slab[(((size_t)chunk * g.T + i) * FR + fb * 16 + 4 * g4 + r) * g.Opad + oo] = acc[fb][r];
   }
 #pragma unroll
   for (int kj = 0; kj < NKJ; ++kj) {
     float q = qa[kj];
     q += __shfl_xor(q, 16);
     q += __shfl_xor(q, 32);
-    if (g4 == 0) ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + o] = q;
+    if (g4 == 0) ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + oo] = q;
   }
 }
 
@@ -377,11 +485,15 @@ template <int NBW, int NBA>
 int launch_dense_fwd_n(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s) {
   CtxLayout L = ctx_layout(g);
   auto kern = g.KS == 1 ? dense_fwd_kernel<NBW, NBA, 1> : dense_fwd_kernel<NBW, NBA, 2>;
+  auto klit = g.KS == 1 ? dense_fwd_lit_kernel<NBW, NBA, 1> : dense_fwd_lit_kernel<NBW, NBA, 2>;
+  const uint8_t* wr = wreg(g, ctx);
+  uint2* st = reinterpret_cast<uint2*>(ctx + L.st);
   const int slot = prof_begin(KID_FWD, g, s);
   hipLaunchKernelGGL(kern, dim3(g.M / 64, g.O / 64), dim3(256), 0, s, g, ctx + L.xcode,
-                     reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag), params_of(g, ctx), sw, sa, out,
-                     reinterpret_cast<uint2*>(ctx + L.st));
+                     reinterpret_cast<const v4i*>(wr + L.wfrag), params_of(g, ctx), sw, sa, out, st);
   prof_end(slot, s);
+  hipLaunchKernelGGL(klit, dim3(32), dim3(256), 0, s, g, ctx + L.xcode, reinterpret_cast<const v4i*>(wr + L.wfrag),
+                     params_of(g, ctx), sw, sa, out, st);
   return check_hip("dense_fwd");
 }
 
@@ -394,14 +506,14 @@ int launch_dense_bwd_n(const Geo& g, const uint8_t* ctx, const float* sw, const 
   const uint2* st = reinterpret_cast<const uint2*>(ctx + L.st);
   {
     const int slot = prof_begin(KID_BWD_GX, g, s);
-    hipLaunchKernelGGL((dense_gx_kernel<NBW, NBA>), dim3(g.M / 128, g.T), dim3(256), 0, s, g, st,
+    hipLaunchKernelGGL((dense_gx_kernel<NBW, NBA>), dim3(g.M / 128, g.T), dim3(512), 0, s, g, st,
                        reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wgx), pp, sw, gout, gx);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("dense_gx"));
   }
   {
     const int slot = prof_begin(KID_BWD_GW, g, s);
-    hipLaunchKernelGGL((dense_gw_kernel<NBW, NBA>), dim3(W.nchunks_bwd, g.T, g.O / 64), dim3(256), 0, s, g,
+    hipLaunchKernelGGL((dense_gw_kernel<NBW, NBA>), dim3(W.nchunks_bwd, g.T, cdiv(g.O, 128)), dim3(512), 0, s, g,
                        dense_rows_per_chunk(g), st, ctx + L.xhat, pp, gout, reinterpret_cast<float*>(ws + W.gw_slab),
                        reinterpret_cast<float*>(ws + W.ga_slab));
     prof_end(slot, s);
