@@ -213,78 +213,99 @@ __global__ __launch_bounds__(256) void dense_fwd_lit_kernel(Geo g, const uint8_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// grad_x: block = 128 rows x one crossbar tile (<= 8 blocks of 16 channels), 8 waves.  Per K-step
-// of 32 kappa = (k, o) the whole block builds the A operand G_i[m, kappa] = g[m, o] * E_ik[m, o]
-// (hi / mid / lo bf16) into LDS -- wave w the rows 16w..16w+15, each lane one MFMA fragment -- and
-// wave w then multiplies rows 32(w&3)..+31 by the channel blocks 4(w>>2)..+3, the B fragments (the
-// int8 ctx weight slices as bf16, wgx_item layout) read from global one step ahead.  K-steps run
-// o-pair major, slice k minor, so a lane loads each of its state words and g values once.
+// grad_x: block = 128 rows x one crossbar tile (<= 8 blocks of 16 channels), 16 waves in two roles.
+// Per K-step of 32 kappa = (k, o): the 8 builder waves (8..15) write the A operand
+// G_i[m, kappa] = g[m, o] * E_ik[m, o] of the NEXT step (hi / mid / lo bf16) into LDS -- builder b
+// the rows 16b..16b+15, each lane one MFMA fragment -- while the 8 MFMA waves (0..7) multiply this
+// step's G, rows 32(w&3)..+31, by the channel blocks 4(w>>2)..+3 (B: the int8 ctx weight slices as
+// bf16, wgx_item layout, read from global one step ahead).  One barrier per step; the two roles
+// share each SIMD (4 waves), so the split products and the MFMAs overlap.  K-steps run o-pair
+// major, slice k minor: a builder lane loads each of its state words and g values once, one o-pair
+// ahead.
 // ---------------------------------------------------------------------------------------------
 template <int NBW, int NBA>
-__global__ __launch_bounds__(512) void dense_gx_kernel(Geo g, const uint2* __restrict__ st, const v4i* __restrict__ wgx,
-                                                       Params pp, const float* __restrict__ sw_p,
-                                                       const float* __restrict__ gout, float* __restrict__ gx) {
+__global__ __launch_bounds__(1024) void dense_gx_kernel(Geo g, const uint2* __restrict__ st, const v4i* __restrict__ wgx,
+                                                        Params pp, const float* __restrict__ sw_p,
+                                                        const float* __restrict__ gout, float* __restrict__ gx) {
   constexpr int NKJ = NBW * NBA;
   __shared__ v4i Gs[2 * 3 * 8 * 64];  // [buffer][hi/mid/lo][16-row block][lane]
   __shared__ float cel[NKJ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int m0 = blockIdx.x * 128, i = blockIdx.y;
-  const int rg = wave & 3, chh = wave >> 2;
-  for (int t = threadIdx.x; t < NKJ; t += 512) cel[t] = pp.ckj[NKJ + t];
+  const bool builder = wave >= 8;
+  for (int t = threadIdx.x; t < NKJ; t += 1024) cel[t] = pp.ckj[NKJ + t];
   __syncthreads();
-  bool std_mask;  // cE_kj = 2^(bsw*k) for every j: E_k = 2^(bsw*k) * popcount(pass bits of slice k)
-  {
-    const int kl = lane < NKJ ? lane / NBA : 0;
-    std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cel[lane < NKJ ? lane : 0] != ldexpf(1.f, g.bsw * kl)) == 0ull;
-  }
-  // builder: row m0 + 16 wave + r16, kappa channels 32p + 4g4 + e (e < 4) and 32p + 16 + 4g4 + e
-  const size_t mb = (size_t)m0 + 16 * wave + r16;
-  const uint2* strow = st + ((size_t)i * g.M + mb) * g.O + 4 * g4;
-  const float* grow = gout + mb * g.O + 4 * g4;
-  uint32_t pw[8];
-  float gv[8];
-  auto load_p = [&](int p) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(strow + 32 * p);
-    const uint4 a0 = s4[0], a1 = s4[1], b0 = s4[8], b1 = s4[9];
-    pw[0] = a0.y; pw[1] = a0.w; pw[2] = a1.y; pw[3] = a1.w;  // pass bits
-    pw[4] = b0.y; pw[5] = b0.w; pw[6] = b1.y; pw[7] = b1.w;
-    const float4 ga = *reinterpret_cast<const float4*>(grow + 32 * p);
-    const float4 gb = *reinterpret_cast<const float4*>(grow + 32 * p + 16);
-    gv[0] = ga.x; gv[1] = ga.y; gv[2] = ga.z; gv[3] = ga.w;
-    gv[4] = gb.x; gv[5] = gb.y; gv[6] = gb.z; gv[7] = gb.w;
-  };
-  auto build = [&](int k, int buf) {
-    float Gv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float E;
-      if (std_mask) {
-        E = ldexpf((float)__popc(pw[e] & dmask_k(k, NBA)), g.bsw * k);
-      } else {
-        E = 0.f;
-#pragma unroll
-        for (int j = 0; j < NBA; ++j) E += ((pw[e] >> (k * NBA + j)) & 1u) ? cel[k * NBA + j] : 0.f;
-      }
-      Gv[e] = gv[e] * E;
-    }
-    v8bf h, md, lo;
-    split3x8(Gv, h, md, lo);
-    v4i* dst = Gs + (buf * 3 * 8 + wave) * 64 + lane;
-    dst[0] = as_v4i(h);
-    dst[8 * 64] = as_v4i(md);
-    dst[16 * 64] = as_v4i(lo);
-  };
   const int hp = g.OB16 / 2;  // o-pairs (O % 64 == 0)
   const int nsteps = NBW * hp;
+  if (builder) {
+    bool std_mask;  // cE_kj = 2^(bsw*k) for every j: E_k = 2^(bsw*k) * popcount(pass bits of slice k)
+    {
+      const int kl = lane < NKJ ? lane / NBA : 0;
+      std_mask = __builtin_amdgcn_ballot_w64(lane < NKJ && cel[lane < NKJ ? lane : 0] != ldexpf(1.f, g.bsw * kl)) == 0ull;
+    }
+    const int bw = wave - 8;
+    // row m0 + 16 bw + r16, kappa channels 32p + 4g4 + e (e < 4) and 32p + 16 + 4g4 + e
+    const size_t mb = (size_t)m0 + 16 * bw + r16;
+    const uint2* strow = st + ((size_t)i * g.M + mb) * g.O + 4 * g4;
+    const float* grow = gout + mb * g.O + 4 * g4;
+    uint4 sa0, sa1, sb0, sb1, na0, na1, nb0, nb1;
+    float4 ga, gb, nga, ngb;
+    auto load_p = [&](int p, uint4& a0, uint4& a1, uint4& b0, uint4& b1, float4& fa, float4& fb) {
+      const uint4* s4 = reinterpret_cast<const uint4*>(strow + 32 * p);
+      a0 = s4[0]; a1 = s4[1]; b0 = s4[8]; b1 = s4[9];
+      fa = *reinterpret_cast<const float4*>(grow + 32 * p);
+      fb = *reinterpret_cast<const float4*>(grow + 32 * p + 16);
+    };
+    auto build = [&](int k, int buf) {
+      const uint32_t pw[8] = {sa0.y, sa0.w, sa1.y, sa1.w, sb0.y, sb0.w, sb1.y, sb1.w};  // pass bits
+      const float gv[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+      float Gv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float E;
+        if (std_mask) {
+          E = ldexpf((float)__popc(pw[e] & dmask_k(k, NBA)), g.bsw * k);
+        } else {
+          E = 0.f;
+#pragma unroll
+          for (int j = 0; j < NBA; ++j) E += ((pw[e] >> (k * NBA + j)) & 1u) ? cel[k * NBA + j] : 0.f;
+        }
+        Gv[e] = gv[e] * E;
+      }
+      v8bf h, md, lo;
+      split3x8(Gv, h, md, lo);
+      v4i* dst = Gs + (buf * 3 * 8 + bw) * 64 + lane;
+      dst[0] = as_v4i(h);
+      dst[8 * 64] = as_v4i(md);
+      dst[16 * 64] = as_v4i(lo);
+    };
+    load_p(0, sa0, sa1, sb0, sb1, ga, gb);
+    if (hp > 1) load_p(1, na0, na1, nb0, nb1, nga, ngb);
+    build(0, 0);
+    __syncthreads();
+    for (int t = 0; t < nsteps; ++t) {
+      const int tn = t + 1;
+      if (tn < nsteps) {
+        const int k = tn % NBW;
+        if (k == 0) {  // next o-pair: its words arrived during the last NBW steps; fetch the one after
+          sa0 = na0; sa1 = na1; sb0 = nb0; sb1 = nb1; ga = nga; gb = ngb;
+          const int pn = tn / NBW + 1;
+          if (pn < hp) load_p(pn, na0, na1, nb0, nb1, nga, ngb);
+        }
+        build(k, tn & 1);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  const int rg = wave & 3, chh = wave >> 2;
   auto step_s = [&](int t) { return (t % NBW) * hp + t / NBW; };
   const int nf = min(4, g.FBT - 4 * chh);  // this wave's channel blocks (0 when the tile has 4)
   const v4i* wt = wgx + ((size_t)i * g.FBT + 4 * chh) * g.NKS * 64 + lane;
   v4i bc[4], bn[4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) bc[f] = f < nf ? wt[((size_t)f * g.NKS + step_s(0)) * 64] : v4i{0, 0, 0, 0};
-  load_p(0);
-  build(0, 0);
   __syncthreads();
   v4f acc[2][4];
 #pragma unroll
@@ -297,7 +318,6 @@ __global__ __launch_bounds__(512) void dense_gx_kernel(Geo g, const uint2* __res
       const int sn = step_s(tn);
 #pragma unroll
       for (int f = 0; f < 4; ++f) bn[f] = f < nf ? wt[((size_t)f * g.NKS + sn) * 64] : v4i{0, 0, 0, 0};
-      if (tn % NBW == 0) load_p(tn / NBW);
     }
     if (nf > 0) {
 #pragma unroll
@@ -306,14 +326,13 @@ __global__ __launch_bounds__(512) void dense_gx_kernel(Geo g, const uint2* __res
         const v8bf ah = as_v8bf(src[0]), am = as_v8bf(src[8 * 64]), al = as_v8bf(src[16 * 64]);
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          const v8bf bw = as_v8bf(bc[f]);
-          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bw, acc[h][f], 0, 0, 0);
-          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bw, acc[h][f], 0, 0, 0);
-          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bw, acc[h][f], 0, 0, 0);
+          const v8bf bwv = as_v8bf(bc[f]);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bwv, acc[h][f], 0, 0, 0);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bwv, acc[h][f], 0, 0, 0);
+          acc[h][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bwv, acc[h][f], 0, 0, 0);
         }
       }
     }
-    if (tn < nsteps) build(tn % NBW, tn & 1);
     __syncthreads();
 #pragma unroll
     for (int f = 0; f < 4; ++f) bc[f] = bn[f];
@@ -506,7 +525,7 @@ int launch_dense_bwd_n(const Geo& g, const uint8_t* ctx, const float* sw, const 
   const uint2* st = reinterpret_cast<const uint2*>(ctx + L.st);
   {
     const int slot = prof_begin(KID_BWD_GX, g, s);
-    hipLaunchKernelGGL((dense_gx_kernel<NBW, NBA>), dim3(g.M / 128, g.T), dim3(512), 0, s, g, st,
+    hipLaunchKernelGGL((dense_gx_kernel<NBW, NBA>), dim3(g.M / 128, g.T), dim3(1024), 0, s, g, st,
                        reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wgx), pp, sw, gout, gx);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("dense_gx"));
