@@ -407,7 +407,10 @@ def _prep_key(desc, lsq, x_shape):
 
 
 def _versions(*ts):
-    return tuple(-1 if t is None else t._version for t in ts)
+    """Staleness key of a prepared weight side: each tensor's version counter and storage
+    address.  An edit through ``p.data`` bumps neither; after one, call prepare_weights again
+    (or torch.autograd.graph.increment_version(p)) before the next forward."""
+    return tuple(-1 if t is None else (t._version, t.data_ptr()) for t in ts)
 
 
 def _module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits,

@@ -135,8 +135,26 @@ def build_model(hp, device):
     arch = f"{hp.arch}_Conv2dLSQCiM"
     if hp.HasField("resume") and os.path.isfile(hp.resume):
         ck = torch.load(hp.resume, map_location="cpu", weights_only=True)
-        model.load_state_dict(ck.get("state_dict", ck), strict=False)
+        load_resume_state(model, ck.get("state_dict", ck))
     return model.to(device), arch
+
+
+def load_resume_state(model, state):
+    """Resume from a checkpoint written here (the bare model's keys) or by the reference's
+    main_lsq.py under DDP (main_lsq.py:121 saves the wrapped model, keys prefixed 'module.').
+    The prefix is stripped or added to match ``model``; non-strict like the reference's resume,
+    but a checkpoint none of whose keys match is an error rather than a silent no-op."""
+    own = model.state_dict().keys()
+    wrapped = any(k.startswith("module.") for k in own)
+    fixed = {}
+    for k, v in state.items():
+        bare = k[len("module."):] if k.startswith("module.") else k
+        fixed[("module." + bare) if wrapped else bare] = v
+    res = model.load_state_dict(fixed, strict=False)
+    if fixed and len(res.unexpected_keys) == len(fixed):
+        raise RuntimeError("resume: no checkpoint key matches the model (%d keys, e.g. %r)"
+                           % (len(fixed), next(iter(fixed))))
+    return res
 
 
 def accuracy(output, target, topk=(1,)):

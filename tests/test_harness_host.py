@@ -164,3 +164,23 @@ def test_checkpoint_round_trip(tmp_path):
     m2 = models.resnet20()
     m2.load_state_dict(ck["state_dict"])
     assert all(torch.equal(a, b) for a, b in zip(model.state_dict().values(), m2.state_dict().values()))
+
+
+def test_resume_accepts_reference_ddp_keys():
+    """main_lsq.py:121 saves the DDP-wrapped model ('module.' keys); resume strips or adds the
+    prefix to match, and a checkpoint with no matching key is an error, not a silent no-op."""
+    src = models.resnet20()
+    ddp_state = {"module." + k: v for k, v in src.state_dict().items()}
+    dst = models.resnet20()
+    train.load_resume_state(dst, ddp_state)
+    assert all(torch.equal(a, b) for a, b in zip(src.state_dict().values(), dst.state_dict().values()))
+
+    class Wrap(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.module = m
+    wrapped = Wrap(models.resnet20())
+    train.load_resume_state(wrapped, src.state_dict())
+    assert all(torch.equal(a, b) for a, b in zip(src.state_dict().values(), wrapped.module.state_dict().values()))
+    with pytest.raises(RuntimeError, match="no checkpoint key"):
+        train.load_resume_state(models.resnet20(), {"foo.bar": torch.zeros(1)})
