@@ -194,6 +194,54 @@ def timed_forward(trainer, xs, steps, dev, world, graph):
     return time.perf_counter() - t0
 
 
+def step_context(batch, world, ms_step, ms_fwd):
+    """SURVEY 8(d) / BASELINE.md rates of the 19 layers: bit-sliced MAC/s of the forward (logical MAC x
+    nbw x nba, the products the crossbar model computes) and algorithmic HBM GB/s of fwd+bwd (per layer
+    forward 4(|x|+|y|), grad_x 8|x|+4|y|, grad_w 4(|x|+|y|) bytes)."""
+    bs_mac = 0.0
+    byts = 0.0
+    for _, c, o, h, s, nb in RESNET20:
+        ho = out_hw(h, s)
+        bs_mac += batch * ho * ho * o * c * 9 * nb * nb
+        nx, ny = batch * c * h * h, batch * o * ho * ho
+        byts += 16.0 * nx + 12.0 * ny
+    return {"bit_sliced_mac_per_s_fwd": bs_mac * world / (ms_fwd * 1e-3),
+            "algorithmic_hbm_gb_per_s_fwd_bwd": byts * world / (ms_step * 1e-3) / 1e9,
+            "algorithmic_bytes_per_step_per_gpu": byts}
+
+
+def measured_peaks(dev):
+    """Attainable peaks on this box, beside the spec peaks the roofline uses: a 4 GiB device copy
+    (read + write bytes / time) and a 8192^3 bf16 torch.matmul (hipBLASLt)."""
+    res = {}
+    n = 1 << 30
+    a = torch.empty(n, device=dev, dtype=torch.float32)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    res["hbm_copy_gb_per_s"] = 10 * 2 * 4.0 * n / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    m = 8192
+    x = torch.randn(m, m, device=dev, dtype=torch.bfloat16)
+    y = torch.randn(m, m, device=dev, dtype=torch.bfloat16)
+    torch.matmul(x, y)
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(10):
+        torch.matmul(x, y)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    res["bf16_matmul_tflop_per_s"] = 10 * 2.0 * m ** 3 / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    res["spec"] = {"hbm_gb_per_s": PEAK_HBM_GBS, "bf16_tflop_per_s": PEAK_BF16_TFLOPS, "i8_top_per_s": PEAK_I8_TOPS}
+    return res
+
+
 def source_sha():
     """sha256 of the kernel sources: ties a committed PMC traffic file to the kernels it measured."""
     import glob
@@ -402,6 +450,7 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=256)
     ap.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE cfg5 (QuantLinear) extra line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the measured HBM-copy / bf16-GEMM peaks")
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from the host each step")
     args = ap.parse_args()
 
@@ -506,7 +555,10 @@ def main():
                          traffic_source=traffic_source),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
+        "rates": step_context(args.batch, world, ms_per_step, fwd_elapsed / args.steps * 1e3),
     }
+    if world == 1 and not args.no_peaks:
+        result["peaks_measured"] = measured_peaks(dev)
     if world == 1 and not args.no_cfg5:
         ex = {"cfg5": bench_cfg5(dev, args.steps, args.warmup)}
         one = [("layer", 16, 16, 32, 1, 3)]

@@ -31,15 +31,18 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     CIMQ_TRY(check_hip("prep_wfrag"));
   }
   if (need_wgx) {
-    int total = g.T * g.FBT * g.NKS * 64;
-    hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
-                       reinterpret_cast<v4i*>(wreg(g, ctx) + L.wgx));
-    const int Cp = (g.C + 15) / 16 * 16;
-    const int tw = g.T * g.KHW * Cp * g.NKS * 4;
-    hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
-                       reinterpret_cast<uint4*>(wreg(g, ctx) + L.wtc));
-    CIMQ_TRY(check_hip("prep_wgx"));
     const Plan7 p7 = v7_plan(g);
+    // the general / v6 grad_x operands only where the v7 backward will not run
+    if (!(p7.ok && (g.variant == VAR_LIBRARY || shift_stats_ok(g)))) {
+      int total = g.T * g.FBT * g.NKS * 64;
+      hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
+                         reinterpret_cast<v4i*>(wreg(g, ctx) + L.wgx));
+      const int Cp = (g.C + 15) / 16 * 16;
+      const int tw = g.T * g.KHW * Cp * g.NKS * 4;
+      hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
+                         reinterpret_cast<uint4*>(wreg(g, ctx) + L.wtc));
+      CIMQ_TRY(check_hip("prep_wgx"));
+    }
     if (p7.ok) {
       const int tc = g.T * p7.v.NCPBT * g.NKS * 64;
       hipLaunchKernelGGL(prep_wcy_kernel, dim3(cdiv(tc, blk)), dim3(blk), 0, s, g, w_q, sw, p7.v.NCPBT,
@@ -50,7 +53,7 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   Params pp = params_of(g, ctx);
   if (need_params) {
     if (hipMemsetAsync(pp.flags, 0, 16, s) != hipSuccess) return fail(CIMQ_EHIP, "memset flags");
-    int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+    int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba + (beta != nullptr ? g.Opad : 0);
     hipLaunchKernelGGL(prep_params_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, alpha_q, sw, sa,
                        bmask, pp, beta);
     CIMQ_TRY(check_hip("prep_params"));
@@ -166,7 +169,7 @@ int cimq_shift_backward(const cimq_conv_desc* d, const float* grad_out, const fl
                         float* grad_alpha, float* grad_beta, float* grad_sa, void* ws, void* stream) {
   Geo g;
   CIMQ_TRY(make_geo(d, &g));
-  (void)alpha; (void)beta; (void)binary_mask;
+  (void)alpha; (void)beta;
   if (g.variant != VAR_SHIFT_ROUND && g.variant != VAR_SHIFT_SIGN)
     return fail(CIMQ_EINVAL, "cimq_shift_backward needs adc_variant CIMQ_ADC_SHIFT_ROUND or _SIGN");
   if (!grad_out || !sa || !sw || !signed_act || !ctx || !grad_x || !grad_w || !grad_alpha || !grad_beta || !ws)
@@ -177,6 +180,25 @@ int cimq_shift_backward(const cimq_conv_desc* d, const float* grad_out, const fl
   const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
   uint8_t* w = reinterpret_cast<uint8_t*>(ws);
   bool lsq_fused = false;
+  if (v7_plan(g).ok && shift_stats_ok(g)) {
+    // the shift ADC on the fast path (shift_fast): grad_x / grad_w from the state words as for the
+    // library ADC (same STE mask), the step-size gradients from the statistics kernel
+    if (!binary_mask) return fail(CIMQ_EINVAL, "null binary_mask");
+    CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
+    WsLayout W = ws_layout(g);
+    const long long nout = (long long)g.T * g.FBT * 16 * g.Opad;
+    hipLaunchKernelGGL(reduce_gw_v3_kernel, dim3(cdiv(nout, 64)), dim3(1024), 0, s, g, W.nchunks_bwd,
+                       reinterpret_cast<const float*>(w + W.gw_slab), sa, grad_w);
+    CIMQ_TRY(check_hip("reduce_gw"));
+    CIMQ_TRY(launch_shift_stats(g, c, sw, sa, grad_out, binary_mask, w, grad_alpha, grad_beta, s));
+    if (g.input_kind == CIMQ_INPUT_RAW_LSQ) {
+      if (!lsq_fused) return fail(CIMQ_EINVAL, "internal: unfused act-LSQ backward on the v7 path");
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, g.B * v7_plan(g).v.nbands,
+                         reinterpret_cast<float*>(w + W.lsq_part), grad_sa);
+      CIMQ_TRY(check_hip("sum_partials"));
+    }
+    return CIMQ_OK;
+  }
   CIMQ_TRY(launch_bwd_general(g, c, sw, sa, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
   WsLayout W = ws_layout(g);
   {

@@ -57,6 +57,7 @@ struct Params {
   float* ckj;   // [3][nbw*nba]: mask as float, cE = 2^-(bsa*j)*mask, cD = 2^-(bsw*k)*mask
   int* flags;   // [0]: literal ADC (degenerate alpha / scales), [1..3] reserved
   float* beta;  // shift of the scale + shift ADC variants (0 otherwise)
+  float* bsum;  // [Opad]: sum over (i, k, j) of beta * binary_mask (shift_fast forward)
 };
 
 __host__ __device__ inline int pidx(const Geo& g, int i, int j, int k, int o) {
@@ -183,6 +184,14 @@ __device__ inline bool has_alpha(const Geo& g) {
   return g.mode == ADC_SIGN || g.mode == ADC_TERNARY || g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN;
 }
 __device__ inline bool is_shift(const Geo& g) { return g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN; }
+// The scale / shift "round" ADC of Conv2dLSQCiM(adc_shift=True) on the threshold fast path: 1.5 bits
+// with the library's range (codes -1, 0, 1), the library's fp16 partial sums (no int8 buffer), every
+// |ps| exact in fp16.  v = (u - beta) / alpha is then a monotone step function of the integer ps,
+// captured by integer thresholds like the library ADC; the output gains sum beta * mask per channel.
+__host__ __device__ inline bool shift_fast(const Geo& g) {
+  return g.variant == VAR_SHIFT_ROUND && g.mode == ADC_TERNARY && !g.ps_int8 && g.qp == 1.f && g.qn == -1.f &&
+         g.psmax <= 2048;
+}
 
 // torch.sign: NaN propagates
 __device__ inline float sign_nan(float v) { return (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : ((v != v) ? v : 0.f)); }

@@ -8,6 +8,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -152,7 +154,7 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
@@ -173,6 +175,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.coef = o; o = align256(o + npar * 4);
   L.alpha = o; o = align256(o + npar * 4);
   L.beta = o; o = align256(o + npar * 4);
+  L.bsum = o; o = align256(o + (size_t)g.Opad * 4);
   L.ckj = o; o = align256(o + 3 * 64 * 4);
   L.flags = o; o = align256(o + 16);
   L.lsq_scal = o; o = align256(o + 16 * 4);
@@ -207,6 +210,7 @@ inline Params params_of(const Geo& g, uint8_t* ctx) {
   p.coef = reinterpret_cast<float*>(base + L.coef);
   p.alpha = reinterpret_cast<float*>(base + L.alpha);
   p.beta = reinterpret_cast<float*>(base + L.beta);
+  p.bsum = reinterpret_cast<float*>(base + L.bsum);
   p.ckj = reinterpret_cast<float*>(base + L.ckj);
   p.flags = reinterpret_cast<int*>(base + L.flags);
   return p;
@@ -253,7 +257,9 @@ inline Plan3 v3_plan(const Geo& g) {
   Plan3 p;
   memset(&p, 0, sizeof(p));
   if (tune("V3", 1) == 0) return p;  // experiments: force the general kernels
-  if (g.variant != VAR_LIBRARY) return p;  // ADC variants: literal per-partial-sum evaluation
+  // ADC variants: literal per-partial-sum evaluation on the general kernels, except the shift ADC
+  // whose thresholds the params kernel finds like the library's (shift_fast)
+  if (g.variant != VAR_LIBRARY && !shift_fast(g)) return p;
   if (g.P % 64 != 0 || g.Wo > 64 || 64 % g.Wo != 0 || g.Wo < 4) return p;
   if (g.O > 256 || 256 % g.O != 0) return p;  // grad_alpha reducer: one thread per channel
   if ((g.W * g.NBP) % 16 != 0 || g.KS > 2 || g.FBT > 8) return p;
@@ -333,6 +339,68 @@ struct Plan7 {
   int pairs;
 };
 
+// grad_w LDS plane pitches.  A row group's A fragment: lane l reads 16 B (8 bf16) at plane
+// kw*KWP + channel c*CPITCH + staged row (oh*SH + kh)*Wo + ow0, for row f = 16*gr + (l & 15) =
+// (c, kh, kw) and pixels 32*wave + 8*(l >> 4) of the stage.  ds_read_b128 serves a wave in 4 fixed
+// groups of 16 lanes, one LDS cycle per distinct address on a busy 16-B slot of the 256-B bank row
+// (MI355X_MICROARCH.md, LDS).  The unpadded pitches (CPITCH = NSLOT*Wo + 8, KWP = CPL*CPITCH) put
+// the three kw planes of a row on one slot: 140 cycles per stage-wave where 36 is the floor.
+inline int gw_read_cycles(const Geo& g, const V7& v, int cp, int kwp) {
+  static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  int cyc = 0;
+  for (int wave = 0; wave < 4; ++wave)
+    for (int gr = 0; gr * 16 < v.CPL * g.KHW; ++gr)
+      for (int q = 0; q < 4; ++q) {
+        int addr[16], slot[16];
+        for (int t = 0; t < 16; ++t) {
+          const int l = grp[q][t], f = 16 * gr + (l & 15);
+          const int c = f / g.KHW, tap = f - c * g.KHW, kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int moff = 32 * wave + 8 * (l >> 4);
+          const int img = v.whole ? moff / g.P : 0, pim = v.whole ? moff % g.P : moff;
+          addr[t] = c < v.CPL ? kw * kwp + c * cp + (img * g.H + (pim / g.Wo) * g.SH + kh) * g.Wo + pim % g.Wo : -1;
+          slot[t] = addr[t] < 0 ? -1 : (addr[t] / 8) % 16;  // rows past CPL read one zero pad (broadcast)
+        }
+        int worst = 1;
+        for (int s = 0; s < 16; ++s) {
+          int n = 0;
+          for (int t = 0; t < 16; ++t) {
+            if (slot[t] != s) continue;
+            bool dup = false;
+            for (int u = 0; u < t; ++u) dup = dup || addr[u] == addr[t];
+            n += dup ? 0 : 1;
+          }
+          worst = std::max(worst, n);
+        }
+        cyc += worst;
+      }
+  return cyc;
+}
+// pads in 8-element (16-B) steps -- CPITCH by up to 24, KWP by up to 120 elements (<= 10 % more LDS) --
+// with the fewest read cycles, then the smallest planes; cached per geometry
+inline void gw_pitches(const Geo& g, V7& v) {
+  static std::mutex mu;
+  static std::map<std::array<int, 8>, std::pair<int, int>> memo;
+  const std::array<int, 8> key = {g.C, g.H, g.Wo, g.P, g.SH, g.KHW, v.NSLOT, v.whole};
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = memo.find(key);
+  if (it == memo.end()) {
+    const int cp0 = v.NSLOT * g.Wo + 8;
+    int best = -1, bcp = cp0, bkwp = v.CPL * cp0;
+    for (int a = 0; a < 4; ++a)
+      for (int b = 0; b < 16; ++b) {
+        const int cp = cp0 + 8 * a, kwp = v.CPL * cp + 8 * b;
+        const int c = tune("GW_PAD", 1) ? gw_read_cycles(g, v, cp, kwp) : (a + b == 0 ? 0 : 1);
+        if (best < 0 || c < best || (c == best && kwp < bkwp)) { best = c; bcp = cp; bkwp = kwp; }
+      }
+    it = memo.emplace(key, std::make_pair(bcp, bkwp)).first;
+  }
+  v.CPITCH = it->second.first;
+  v.KWP = it->second.second;
+}
+
 inline Plan7 v7_plan(const Geo& g) {
   Plan7 p;
   memset(&p, 0, sizeof(p));
@@ -391,8 +459,8 @@ inline Plan7 v7_plan(const Geo& g) {
   }
   // grad_w
   v.NSLOT = v.whole ? (128 / g.P) * g.H : ((128 / g.Wo) - 1) * g.SH + g.KH;
-  v.CPITCH = v.NSLOT * g.Wo + 8;
   v.CPL = std::min(16, g.C);
+  gw_pitches(g, v);
   // tiles touching one channel block (the kernel's loop takes at most 3)
   v.NTL = 1;
   for (int cb = 0; cb * 16 < g.C; ++cb) {
@@ -400,7 +468,7 @@ inline Plan7 v7_plan(const Geo& g) {
     v.NTL = std::max(v.NTL, ihi - ilo + 1);
   }
   if (v.NTL > 3) return p;
-  const size_t planes = (size_t)g.nba * g.KW * v.CPL * v.CPITCH * 2;
+  const size_t planes = (size_t)g.nba * g.KW * v.KWP * 2;
   p.lds_gw = std::max(a16(planes), (size_t)4 * 9 * 256 * 4) + 64 * 4 + (size_t)4 * v.NTL * g.nbw * g.nba * 16 * 4;
   if (g.SH == 1 && v.CPL * v.NSLOT * (g.Wo / 8) > 512) return p;  // grad_w staging: <= 2 items per thread
   p.pairs = ((g.C + 15) / 16) * g.OB16;
@@ -434,9 +502,15 @@ inline int dense_rows_per_chunk(const Geo& g) {
 }
 
 struct WsLayout {
-  size_t gw_slab, ga_slab, gb_slab, lsq_part, gaq, gapart, wpart, bpo, total;
+  size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, total;
   int rows, nchunks, nchunks_bwd;
 };
+
+// pixel chunks of the shift-ADC statistics kernel: about 1024 blocks over (chunks x tiles x o-blocks)
+inline int shift_chunks(const Geo& g) {
+  const int per = std::max(1, 1024 / (g.T * g.OB16));
+  return std::max(1, std::min(per, g.M / 64));
+}
 
 inline WsLayout ws_layout(const Geo& g) {
   WsLayout W;
@@ -451,6 +525,12 @@ inline WsLayout ws_layout(const Geo& g) {
   W.ga_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad);
   W.gb_slab = o; o = align256(o + (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN
                                        ? sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad : 0));
+  // shift ADC on the fast path: per pixel chunk, tile, pair and channel the grad_alpha / grad_beta partials
+  W.ss_slab = o; o = align256(o + (shift_fast(g) ? sizeof(float) * shift_chunks(g) * g.T * 2 * g.nbw * g.nba * g.Opad : 0));
+  // and its q tables [T][OB16][nbw * nba][16][2R + 1] (R = shift_table_range, <= 48 KB per block)
+  W.qtab = o; o = align256(o + (shift_fast(g) ? sizeof(float) * (size_t)g.T * g.OB16 * g.nbw * g.nba * 16 *
+                                                    (2 * std::min(g.K, g.xbar) * ((1 << g.bsa) - 1) * ((1 << g.bsw) - 1) + 1)
+                                              : 0));
   W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * g.H));  // >= B * bands
   // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
   // a [B, P, O] staging copy of out / grad_out for the general kernels
@@ -548,6 +628,13 @@ int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa,
                    float* adc_dbg, hipStream_t s);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
+// shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words
+// (interleaved 3-bit words: w2a2 / w3a3; other slice counts take the general backward)
+inline bool shift_stats_ok(const Geo& g) {
+  return shift_fast(g) && g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
+}
+int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+                       const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s);
 int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
                      hipStream_t s);
 // cimq_part_bwd.hip: backward of layers outside the v7 plan (v5 / v6 and general kernels)

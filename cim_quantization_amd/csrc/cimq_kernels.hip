@@ -490,6 +490,17 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
                                    const float* __restrict__ beta = nullptr) {
   const int npar = g.T * g.nba * g.nbw * g.Opad;
   const int nkj = g.nbw * g.nba;
+  if (t >= npar + nkj) {  // shift ADC: sum_{i,k,j} beta * mask of channel o, added to every output
+    const int o = t - npar - nkj;
+    float b = 0.f;
+    if (beta != nullptr && o < g.O)
+      for (int i = 0; i < g.T; ++i)
+        for (int k = 0; k < g.nbw; ++k)
+          for (int j = 0; j < g.nba; ++j)
+            b += beta[((i * g.nbw + k) * g.nba + j) * g.O + o] * (float)bmask[k * g.nba + j];
+    pp.bsum[o] = b;
+    return false;
+  }
   if (t >= npar) {  // per-(k,j) float coefficients
     const int kj = t - npar, k = kj / g.nba, j = kj - k * g.nba;
     const float mk = (float)bmask[k * g.nba + j];  // binary_mask[0,0,k,j,0,0]
@@ -516,9 +527,27 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
   if (g.mode == ADC_SIGN || g.mode == ADC_TERNARY) {
     if (!(scales_ok(sw, sa) && a > 0.f && isfinite(a))) literal = true;
   }
-  if (g.variant != VAR_LIBRARY) literal = true;  // the variants are evaluated per partial sum
+  // the variants are evaluated per partial sum, except the shift ADC of the fast path
+  const bool sf = shift_fast(g);
+  const float be = pp.beta[t];
+  if (g.variant != VAR_LIBRARY && !sf) literal = true;
+  if (sf && !isfinite(be)) literal = true;
   if (!literal) {
-    if (g.mode == ADC_TERNARY) {
+    if (sf) {
+      // v = (u - beta) / alpha (scale_shift.py:421): code +1 <=> rint(v) >= 1, -1 <=> rint(v) <= -1
+      int L = lo, R = hi + 1;
+      while (L < R) {
+        const int mid = L + ((R - L) >> 1);
+        if (rintf(psb_value(g, mid, sw, sa, a, be)) >= 1.f) R = mid; else L = mid + 1;
+      }
+      thi = L;
+      L = lo - 1; R = hi;
+      while (L < R) {
+        const int mid = L + ((R - L + 1) >> 1);
+        if (rintf(psb_value(g, mid, sw, sa, a, be)) <= -1.f) L = mid; else R = mid - 1;
+      }
+      tlo = L;
+    } else if (g.mode == ADC_TERNARY) {
       thi = first_true_ternary_hi(lo, hi, sw, sa, a);
       tlo = last_true_ternary_lo(lo, hi, sw, sa, a);
     }
@@ -527,14 +556,14 @@ __device__ inline bool params_item(const Geo& g, const ASrc& as, float sw, float
       int L = lo, R = hi + 1;  // first p with psb > thr_lo  (i.e. not "<= thr_lo")
       while (L < R) {
         int mid = L + ((R - L) >> 1);
-        float b = psb_literal(mid, g.mode, sw, sa, a);
+        float b = sf ? psb_value(g, mid, sw, sa, a, be) : psb_literal(mid, g.mode, sw, sa, a);
         if (b > g.thr_lo) R = mid; else L = mid + 1;
       }
       mlo = L;
       L = lo - 1; R = hi;  // last p with psb < thr_hi
       while (L < R) {
         int mid = L + ((R - L + 1) >> 1);
-        float b = psb_literal(mid, g.mode, sw, sa, a);
+        float b = sf ? psb_value(g, mid, sw, sa, a, be) : psb_literal(mid, g.mode, sw, sa, a);
         if (b < g.thr_hi) L = mid; else R = mid - 1;
       }
       mhi = L;
@@ -554,7 +583,7 @@ __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, con
                                    Params pp, const float* __restrict__ beta) {
   const float sw = *sw_p, sa = *sa_p;
   const ASrc as{alpha_q, 0, 0.f, 0.f};
-  const int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
+  const int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba + (beta != nullptr ? g.Opad : 0);
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     if (params_item(g, as, sw, sa, bmask, pp, t, beta)) atomicOr(&pp.flags[0], 1);
 }

@@ -89,10 +89,19 @@ template <int NBP>
 __device__ inline void stage_rows(const Geo& g, int WP, int RHx, const uint8_t* __restrict__ xc, int b,
                                   int ih_first, uint8_t* patch, int c0 = 0, int ncx = -1) {
   const int QW = g.W * NBP / 16;  // 16-byte vectors per row
-  const int n = (ncx < 0 ? g.C : ncx) * RHx * QW;
-  const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
+  const int nrow = (ncx < 0 ? g.C : ncx) * RHx;
+  const int n = nrow * QW;
   const uint4* src = reinterpret_cast<const uint4*>(xc) + ((size_t)b * g.C + c0) * g.H * QW;
   const int nt = blockDim.x;
+  // item -> (row, q) by a shift when QW is a power of two, row -> (c, rr) by a 24-bit
+  // multiply-shift (exact for row * RHx < 2^20); 32-bit offsets from the image's base: no
+  // quarter-rate 32/64-bit multiplies per item
+  const bool pq = (QW & (QW - 1)) == 0;
+  const int lq = 31 - __builtin_clz(QW);
+  const bool mag_ok = nrow * RHx < (1 << 20);
+  const unsigned mag = ((1u << 20) + RHx - 1) / RHx;
+  const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
+  const int HQ = g.H * QW, rowb = WP * NBP, colb = g.PW * NBP;
   for (int base = threadIdx.x; base < n; base += 8 * nt) {
     uint4 v[8];
     int d[8];
@@ -101,12 +110,13 @@ __device__ inline void stage_rows(const Geo& g, int WP, int RHx, const uint8_t* 
       const int idx = base + u * nt;
       d[u] = -1;
       if (idx < n) {
-        const int row = fdiv(idx, QW, invQ), q = idx - row * QW;
-        const int c = fdiv(row, RHx, invR), rr = row - c * RHx;
+        const int row = pq ? (idx >> lq) : fdiv(idx, QW, invQ), q = pq ? (idx & (QW - 1)) : idx - row * QW;
+        const int c = mag_ok ? (int)(__umul24((unsigned)row, mag) >> 20) : fdiv(row, RHx, invR);
+        const int rr = row - c * RHx;
         const int ih = ih_first + rr;
-        d[u] = ((c * RHx + rr) * WP + g.PW) * NBP + q * 16;
+        d[u] = row * rowb + colb + q * 16;
         v[u] = make_uint4(0, 0, 0, 0);
-        if (ih >= 0 && ih < g.H) v[u] = src[((size_t)c * g.H + ih) * QW + q];
+        if ((unsigned)ih < (unsigned)g.H) v[u] = src[c * HQ + ih * QW + q];
       }
     }
 #pragma unroll
@@ -257,6 +267,24 @@ __device__ __noinline__ float code_literal(int p, int mode, float sw, float sa, 
                                            float thr_hi, float thr_lo) {
   const float bb = psb_literal(p, mode, sw, sa, al);
   return alpha_code_literal(bb, mode, qn, qp, thr_hi, thr_lo);
+}
+// the shift ADC's literal path (shift_fast layers with a degenerate alpha / beta / scale): adc * mask
+// (scale_shift.py:421-429) and the state bits of the partial sum (v = (u - beta) / alpha: STE pass
+// unless v >= Qp + 1e-5 or v <= Qn - 1e-5, :469-484; code clamp(rint(v), -1, 1))
+// (scalar arguments only, as the helpers above: a Geo by reference would put it on the stack and
+// cost the whole kernel registers; shift_fast fixes ps_int8 = 0 and the range -1 .. 1)
+__device__ __noinline__ float shift_adc_literal(int p, float sw, float sa, float al, float be, float mk) {
+  const float u = (ps_half(p) * sw) * sa;  // u_var without the int8 buffer
+  const float v = (u - be) / al;
+  const float t = clamp_nan(rintf(v), -1.f, 1.f) * al;
+  return (t + be) * mk;
+}
+__device__ __noinline__ uint32_t shift_state_literal(int p, float sw, float sa, float al, float be, float thr_hi,
+                                                     float thr_lo) {
+  const float v = (((ps_half(p) * sw) * sa) - be) / al;
+  const bool pass = !(v >= thr_hi || v <= thr_lo);
+  const float code = clamp_nan(rintf(v), -1.f, 1.f);
+  return (pass ? 1u : 0u) | ((code != 0.f) ? 2u : 0u) | ((code < 0.f) ? 4u : 0u);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -549,6 +577,21 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                       stw[r] |= ((pass ? 1u : 0u) | ((hi || lo) ? 2u : 0u) | (lo ? 4u : 0u)) << (3 * j);
                     }
                   }
+                } else if (is_shift(g)) {
+                  const float al = pp.alpha[pidx(g, i, j, k, o)], be = pp.beta[pidx(g, i, j, k, o)];
+                  const float mk = ckl[k * g.nba + j];
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    acc[ob][r] += shift_adc_literal(ps[r], sw, sa, al, be, mk);
+                    const uint32_t sb = shift_state_literal(ps[r], sw, sa, al, be, g.thr_hi, g.thr_lo);
+                    if (PLF) {
+                      tq[r][0] |= (sb & 1u) << j;
+                      tq[r][1] |= ((sb >> 1) & 1u) << j;
+                      tq[r][2] |= ((sb >> 2) & 1u) << j;
+                    } else {
+                      stw[r] |= sb << (3 * j);
+                    }
+                  }
                 } else {
                   const float al = pp.alpha[pidx(g, i, j, k, o)];
                   const float mk = ckl[k * g.nba + j];
@@ -624,6 +667,12 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     for (int ob = 0; ob < OBM; ++ob) {
       const int o = (og * OBM + ob) * 16 + r16;
       if (ob < nob && o < g.O) {
+        if (is_shift(g) && !literal) {
+          // the threshold path sums code * alpha * mask; the shift ADC adds beta * mask per pair
+          const float bs = pp.bsum[o];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[ob][r] += bs;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (!g.onchw) out[((size_t)mt * 64 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[ob][r];

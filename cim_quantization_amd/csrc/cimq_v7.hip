@@ -57,6 +57,7 @@ struct V7 {
   int NTL;      // most crossbar tiles touching one 16-channel block (grad_alpha LDS regions)
   int GSH;      // grad_x, NPART > 1, at most 2 o-blocks: the NPART waves of a pixel group build disjoint G chunks and
                 // exchange them through LDS (else every wave builds all of them)
+  int KWP;      // grad_w: (slice j, kw) plane pitch (bf16 elements, >= CPL * CPITCH; gw_pitches)
 };
 
 // pass-bit masks of the state word: all j of slice k / all k of slice j
@@ -460,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   const int i_hi = (min(g.C, cb * 16 + 16) * KHW - 1) / g.xbar;
   const int ntl = i_hi - i_lo + 1;
 
-  const size_t plane = (size_t)CPL * v.CPITCH;  // one (j, kw) plane, bf16 elements
+  const size_t plane = (size_t)v.KWP;  // one (j, kw) plane, bf16 elements (padded: gw_pitches)
   uint8_t* cur = smem;
   __bf16* pl = reinterpret_cast<__bf16*>(cur); { const size_t pb = (size_t)NBA * 3 * plane * 2; cur += al16(pb > 36864 ? pb : (size_t)36864); }
   float* cdl = reinterpret_cast<float*>(cur); cur += 64 * 4;
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
   for (int gr = 0; gr < NGR; ++gr) {
     const int f0 = cb * 16 * KHW + 16 * gr, f = f0 + r16;
     const int c = f / KHW, tap = f - c * KHW, kh = tap / 3, kw = tap - 3 * kh;
-    gpk[gr] = (c < g.C) ? (((kw * CPL + (c - cb * 16)) * v.CPITCH) << 2) | kh : -1;
+    gpk[gr] = (c < g.C) ? ((kw * v.KWP + (c - cb * 16) * v.CPITCH) << 2) | kh : -1;
     gtile[gr] = (f0 < g.C * KHW) ? f0 / g.xbar : -1;
   }
   (void)ca;
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
               const float f1 = (float)(int8_t)xbyte(wv[4 * e2 + 2 + kw], j);
               pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
             }
-            __bf16* dst = pl + ((size_t)(j * 3 + kw) * CPL + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            __bf16* dst = pl + (size_t)(j * 3 + kw) * plane + cl * v.CPITCH + slot * Wo + c8 * 8;
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
               const float f1 = (float)(int8_t)xbyte(pf.w[u2][2 * e2 + 1 + kw], j);
               pk[e2] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);  // exact bf16
             }
-            __bf16* dst = pl + ((size_t)(j * 3 + kw) * CPL + cl) * v.CPITCH + slot * Wo + c8 * 8;
+            __bf16* dst = pl + (size_t)(j * 3 + kw) * plane + cl * v.CPITCH + slot * Wo + c8 * 8;
             *reinterpret_cast<uint4*>(dst) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
         }
