@@ -436,6 +436,27 @@ def bench_layers(dev, specs, batch, xbar, adc, steps, warmup, adc_shift=False, r
     t_f = (time.perf_counter() - t0) / steps
     out = {"ms_fwd_bwd": t_fb * 1e3, "ms_fwd": t_f * 1e3, "fwd_mac_per_s": macs / t_f, "launch": "eager",
            "layers": len(specs), "batch": batch}
+    # the same fwd+bwd replayed as one HIP graph: device time without the host's per-launch cost
+    # (eager timings of these many-small-launch stacks move with the box's host load)
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fb()
+        torch.cuda.current_stream().wait_stream(side)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            fb()
+        gr.replay()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            gr.replay()
+        torch.cuda.synchronize(dev)
+        out["ms_fwd_bwd_graph"] = (time.perf_counter() - t0) / steps * 1e3
+        del gr
+    except Exception as e:  # noqa: BLE001 -- reported, the eager numbers stand
+        out["graph_error"] = f"{type(e).__name__}: {e}"[:200]
     if ref is not None:
         out["reference_cpu_container_ms"] = ref
     return out

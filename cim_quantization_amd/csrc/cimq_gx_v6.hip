@@ -194,17 +194,12 @@ __global__ __launch_bounds__(512, 2) void cim_bwd_gx_v6_kernel(Geo g, V3 v, cons
     const int cb0 = ci0 >> 4;
     const int nr = ((ci1 >> 4) - cb0 + 1) * 16;
     const __bf16* Wb = reinterpret_cast<const __bf16*>(wbuf + (size_t)(n & 1) * WBB);
-#ifndef CIMQ_EXP_NO_DMA
     if (n + 1 < nchunk) {
       issue_states(n + 1);
       issue_w(n + 1);
     }
-#endif
     // phase A: one item = 4 pixels x 4 consecutive kappa (same k, 4 channels), from LDS
     const uint8_t* sb = stb + (size_t)(n & 1) * STB;
-#ifdef CIMQ_EXP_NO_PHASEA
-    if (nquad < 0)
-#endif
     for (int it = threadIdx.x; it < nquad * 8; it += blockDim.x) {
       const int qd = it >> 3, kq = it & 7;
       const int kbl = kq >> 2, kb = 2 * kc + kbl;
@@ -286,9 +281,6 @@ __global__ __launch_bounds__(512, 2) void cim_bwd_gx_v6_kernel(Geo g, V3 v, cons
     // phase B: every owned output tile, every tap
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
-#ifdef CIMQ_EXP_NO_PHASEB
-      if (nquad >= 0) break;
-#endif
       const int t = wave + NW * u;
       const int qb = t / v.CB, cb = t - qb * v.CB;
       if (t < NTb && cb * 16 <= ci1 && cb * 16 + 15 >= ci0) {

@@ -191,12 +191,6 @@ __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, floa
   const float4 v4 = reinterpret_cast<const float4*>(x)[t];
   const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
   uint32_t f[4][NBP / 4], b[4][NBP / 4];
-#ifdef CIMQ_EXP_PREP_NOCOMP
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-#pragma unroll
-    for (int w = 0; w < NBP / 4; ++w) f[e][w] = b[e][w] = __float_as_uint(vv[e]);
-#else
   if (lut) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) act_words_lut<NBP, NBA_C>(g, vv[e], sa, sgn, lut, f[e], b[e]);
@@ -204,7 +198,6 @@ __device__ inline void act_item4(const Geo& g, const float* __restrict__ x, floa
 #pragma unroll
     for (int e = 0; e < 4; ++e) act_words<NBP, NBA_C>(g, vv[e], sa, sgn, f[e], b[e]);
   }
-#endif
   if (NBP == 4) {
     reinterpret_cast<uint4*>(xcf)[t] = make_uint4(f[0][0], f[1][0], f[2][0], f[3][0]);
     reinterpret_cast<uint4*>(xcb)[t] = make_uint4(b[0][0], b[1][0], b[2][0], b[3][0]);

@@ -392,10 +392,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 
   for (int i = 0; i < g.T; ++i) build_ptab(g, i, KS, v.RH, v.WP, ptab + i * KS * 64);
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
-#ifndef CIMQ_EXP_FWD_NOPRO
   if (v.fwd_res)
     for (int i = 0; i < g.T; ++i) stage_tile(i, i);
-#endif
   zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * v.RH * v.WP * NBP / 4);
 
   __syncthreads();
@@ -411,9 +409,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     const int b = fdiv(mt, tiles_per_img, inv_tpi), p0 = (mt - b * tiles_per_img) * 64;
     const int oh0 = p0 >> v.lw;
     __syncthreads();
-#ifndef CIMQ_EXP_FWD_NOSTAGE
     stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
-#endif
     __syncthreads();
     float acc[OBM][4];
 #pragma unroll
@@ -430,11 +426,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;  // K-steps holding data in tile i
       v4i xs[NBP][KS];
       // (the fast path runs every K-step: ptab and the weight operand are zero past the tile)
-#ifdef CIMQ_EXP_FWD_NOGATHER
-      for (int a = 0; a < NBP; ++a) for (int c = 0; c < KS; ++c) xs[a][c] = v4i{lane, a, c, i};
-#else
       gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, (CST > 0 && !literal && std8) ? KS : ksn);
-#endif
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
       const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
@@ -507,10 +499,6 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                 const float cf = ct[pcol];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-#ifdef CIMQ_EXP_FWD_NOADC
-                  acc[ob][r] += (float)ps[j][r] * cf;
-                  continue;
-#endif
                   const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
                   const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
                   const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(ps[j][r] - pv.z) <= (unsigned)pv.w);
@@ -640,11 +628,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
           const int o = (og * OBM + ob) * 16 + r16;
-#ifdef CIMQ_EXP_FWD_NOST
-          if (stc[ob][0] == 0x7fffffffu) {
-#else
           if (ob < nob && o < g.O) {
-#endif
             const size_t e0 = ((size_t)i * g.M + (size_t)mt * 64 + wave * 16 + 4 * g4) * g.O + o;
             if (PLF) {
               uint2* s64 = reinterpret_cast<uint2*>(st);
@@ -1229,9 +1213,6 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
                   }
                 }
               }
-#ifdef CIMQ_EXP_GW_NOQ
-              if (qs == 1234.5f) qacc[kj * 32 + ocol] = qs;
-#else
               if (INIT || has_code) {
                 qs += __shfl_xor(qs, 16);
                 qs += __shfl_xor(qs, 32);
@@ -1241,16 +1222,10 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const u
                   atomicAdd(&qacc[kj * 32 + ocol], qs);
                 }
               }
-#endif
             }
           }
         }
-#ifdef CIMQ_EXP_GW_NOGEMM
-        if (!INIT) gwa[0][ob][0] += D[0][0] + D[NBP - 1][3];
-        if (false) {
-#else
         if (!INIT) {
-#endif
           // B operands (k = (j-pair half h2, pixel r)) for every j-pair, then the f-blocks
           constexpr int NS = NBP / 2;
           v8bf bh[NS], bm[NS], bl[NS];

@@ -132,12 +132,6 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
   }
   const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwt, e4 = e3 + a.nwc, total = e4 + a.npp;
   for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
-#ifdef CIMQ_EXP_PREP_NOFRAG
-    if (t < e4) continue;
-#endif
-#ifdef CIMQ_EXP_PREP_NOPARAMS
-    if (t >= e4) continue;
-#endif
     if (t < e1) wfrag_item(g, ws, a.wfrag, t);
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);
@@ -153,9 +147,6 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
   // (none when the weight side was prepared beforehand: cimq_module_prepare)
   const int nwblk = (int)gridDim.x - a.nact_blocks;
   if ((int)blockIdx.x >= nwblk) {
-#ifdef CIMQ_EXP_PREP_NOACT
-    return;
-#endif
     const float sa = grad_scale_value(a.alpha_act[0], q.gs_a);  // lsq.py:547-548
     const int ab = (int)blockIdx.x - nwblk;
     const bool sgn = a.signed_act[0] != 0.f;
@@ -164,9 +155,6 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
               (long long)a.nact_blocks * blockDim.x, lut);
     return;
   }
-#ifdef CIMQ_EXP_PREP_NOWT
-  return;
-#endif
   module_prep_weights(g, q, a, (int)blockIdx.x, nwblk, red);
 }
 

@@ -280,18 +280,10 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
           if (cb + NPART < ncb) {
 #pragma unroll
             for (int s = 0; s < NKS; ++s) anx[s] = wt[((cb + NPART) * NKS + s) * 64];
-#ifdef CIMQ_EXP_GX_NOWLOAD
-#pragma unroll
-            for (int s = 0; s < NKS; ++s) anx[s] = v4i{lane, s, cb, i};
-#endif
           }
           v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < NKS; ++s) {
-#ifdef CIMQ_EXP_GX_NOMFMA
-            acc[0] += (float)Gh[s][0] + (float)Gm[s][1] + (float)Gl[s][2];
-            continue;
-#endif
             const v8bf a = as_v8bf(acur[s]);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gh[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gm[s], acc, 0, 0, 0);
@@ -307,11 +299,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
             float fp = dpp_from_prev(acc[2]);  // kw = 2 of pixel ow - 1 -> iw = ow
             if (col == 0) fp = 0.f;
             const float y = (acc[1] + fn) + fp;
-#ifdef CIMQ_EXP_GX_NORING
-            if (y == 1234.5f) {
-#else
             if (pv && cp < CPP) {
-#endif
               float* e = rr + cp * RE;
               if (acc_mode) {
                 e[col + 1] += y;
@@ -651,11 +639,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
     for (int u2 = 0; u2 < 2; ++u2) {
       if (SS != 1) break;
       const int it = threadIdx.x + u2 * 256;
-#ifdef CIMQ_EXP_GW_NOSTAGE
-      if (it < 0) {
-#else
       if (it < nit) {
-#endif
         const int cl = it_cl[u2], c8 = it_c8[u2];
         const int slot = v.whole ? it_db[u2] * g.H + it_ih[u2] : it_ih[u2];
 #pragma unroll
@@ -694,11 +678,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
         const int i = i_lo + tl;
         const uint2* s2 = reinterpret_cast<const uint2*>(st) + ((size_t)i * g.M + mk8) * g.O * 3 + (size_t)o * 3;
         const size_t es = (size_t)g.O * 3;
-#ifdef CIMQ_EXP_GW_NOGA
-        if (false) {
-#else
         if (((i * g.xbar) / KHW) / 16 == cb) {
-#endif
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             uint32_t nzw[8], ngw[8];
@@ -747,11 +727,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
-#ifdef CIMQ_EXP_GW_NOD
-            if (true) {
-              D = (float)(uint32_t)ps[e];
-            } else
-#endif
             if (std_mask) {
               const int n = __popcll(ps[e] & m1) - (int)((ps[e] >> nb) & 1ull);
               D = (float)(n * (1 << j));
@@ -772,13 +747,9 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             const bool ok = gpk[gr] >= 0 && sl >= 0;
             const __bf16* src = pl + (size_t)j * 3 * plane + (ok ? (gpk[gr] >> 2) + sl * Wo + ow0 : zoff);
             const v8bf a = as_v8bf(*reinterpret_cast<const v4i*>(src));
-#ifndef CIMQ_EXP_GW_NOMFMA
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc[gr], 0, 0, 0);
-#else
-            acc[gr][0] += (float)a[0] + (float)bh[0] + (float)bm[1] + (float)bq[2];
-#endif
           }
         }
       } else if (!PLS && tl < ntl) {
@@ -792,11 +763,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           for (int e = 0; e < 8; ++e) sv[e] = st[((size_t)i * g.M + mk8 + e) * g.O + o];
         }
         // grad_alpha partials (lsq.py:321-333): sum over the pixels of code * g
-#ifdef CIMQ_EXP_GW_NOGA
-        if (false) {
-#else
         if (((i * g.xbar) / KHW) / 16 == cb) {
-#endif
           float qv[NKJ];
 #pragma unroll
           for (int kj = 0; kj < NKJ; ++kj) {
@@ -862,7 +829,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
           if (gtile[gr] != i) continue;  // uniform: the row groups of tile i
           v4i acur[NBA];
           read_group(gr, acur);
-#ifndef CIMQ_EXP_GW_NOMFMA
 #pragma unroll
           for (int j = 0; j < NBA; ++j) {
             const v8bf a = as_v8bf(acur[j]);
@@ -870,9 +836,6 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[gr], 0, 0, 0);
             acc[gr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[gr], 0, 0, 0);
           }
-#else
-          acc[gr][0] += (float)acur[0][0];
-#endif
         }
       }
     }
