@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -40,6 +40,9 @@ EXPORTED_SYMBOLS = (
     "cimq_module_backward_chain",
     "cimq_pending_flush",
     "cimq_module_prepare",
+    "cimq_module_shift_supported",
+    "cimq_module_shift_forward",
+    "cimq_module_shift_backward",
     "cimq_alpha_init",
     "cimq_shift_forward",
     "cimq_shift_backward",
@@ -161,6 +164,12 @@ def _bind(lib):
     lib.cimq_pending_flush.argtypes = [ctypes.POINTER(Pending), _VP]
     lib.cimq_module_prepare.restype = ctypes.c_int
     lib.cimq_module_prepare.argtypes = [ctypes.c_int, ctypes.POINTER(PrepareItem), _VP]
+    lib.cimq_module_shift_supported.restype = ctypes.c_int
+    lib.cimq_module_shift_supported.argtypes = [ctypes.POINTER(ConvDesc)]
+    lib.cimq_module_shift_forward.restype = ctypes.c_int
+    lib.cimq_module_shift_forward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 12
+    lib.cimq_module_shift_backward.restype = ctypes.c_int
+    lib.cimq_module_shift_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 18
     lib.cimq_alpha_init.restype = ctypes.c_int
     lib.cimq_alpha_init.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 10
     lib.cimq_shift_forward.restype = ctypes.c_int

@@ -18,8 +18,8 @@ import torch
 import torch.nn.functional as F
 
 from ..functional import (alpha_cim_init, cim_conv2d_lsq, cim_conv2d_lsq_shift, cim_module_conv,  # noqa: F401
-                          get_adcless_cim_output, get_analog_partial_sums_autograd_ver2, get_cim_output_signed,
-                          lsq_quantize, qconv2d)
+                          cim_module_shift_conv, get_adcless_cim_output, get_analog_partial_sums_autograd_ver2,
+                          get_cim_output_signed, lsq_quantize, module_shift_supported, qconv2d)
 from ._quan_base import (_ActQ, _Conv2dQ, _Conv2dQCiM, _LinearQ, Qmodes, grad_scale,  # noqa: F401
                          round_pass)
 
@@ -80,6 +80,15 @@ class Conv2dLSQCiM(_Conv2dQCiM):
                 and not self.adc_shift and not self.stochastic_quant and self._last_x_shape is not None
                 and self.weight.is_cuda)
 
+    def _shift_fused(self, x):
+        """Whether libcimq's fused shift path takes input shape x.shape (cached per shape)."""
+        key = tuple(x.shape)
+        if getattr(self, "_shift_ok", None) is None or self._shift_ok[0] != key:
+            self._shift_ok = (key, x.is_cuda and module_shift_supported(
+                key, self.weight, self.stride, self.padding, self.dilation, self.nbits_a, self.abitslice,
+                self.nbits_w, self.wbitslice, self.adcbits, self.xbar, self.nbits_alpha))
+        return self._shift_ok[1]
+
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
         return super()._load_from_state_dict(*args, **kwargs)
@@ -104,6 +113,13 @@ class Conv2dLSQCiM(_Conv2dQCiM):
             flags[0] = True
         if self.binary_mask.device != x.device:
             self.binary_mask = self.binary_mask.to(x.device)
+        if (self.fused and self.adc_shift and flags[0] and flags[1] and self._shift_fused(x)):
+            # steady state of the shift ADC on libcimq's fused path (quantisers in the library)
+            out = cim_module_shift_conv(x, self.weight, self.alpha_act, self.alpha_weight, self.alpha_cim,
+                                        self.beta_cim, self.binary_mask, self.signed_act, self.stride, self.padding,
+                                        self.dilation, self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice,
+                                        self.xbar, self.nbits_alpha)
+            return out if self.bias is None else out + self.bias  # lsq.py:583's broadcast
         if (self.fused and flags[0] and (flags[1] or self.alpha_cim is None) and self.adcbits != 0
                 and not self.adc_shift):
             # steady state: the three quantisers and the CiM conv in one library call each way (the

@@ -318,7 +318,7 @@ static int act_parts(const Geo& g) {
 // the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes
 static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
-                      float* grad_alpha_weight, float* grad_alpha_cim) {
+                      float* grad_alpha_weight, float* grad_alpha_cim, int gaq_ready = 0) {
   const bool has_alpha = la.nbits_alpha > 0;
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
@@ -344,6 +344,7 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   a.napart = act_parts(g);
   a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
   a.gapart = (has_alpha && la.nalpha > kFinishInReg && tune("WIDE_TAIL", 1)) ? reinterpret_cast<float*>(w + W.gapart) : nullptr;
+  a.gaq_ready = gaq_ready;
   j.g = g;
   j.q = la;
   j.tail_blocks = a.nwb + a.nga;
@@ -366,9 +367,9 @@ static int launch_finish(const Carry& j, hipStream_t s) {
 
 static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
                        const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
-                       float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s) {
+                       float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s, int gaq_ready = 0) {
   const Carry j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
-                           grad_alpha_cim);
+                           grad_alpha_cim, gaq_ready);
   CIMQ_TRY(launch_tail(j, s));
   return launch_finish(j, s);
 }
@@ -437,24 +438,31 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
   return a;
 }
 
-// the checks every module entry point shares; applies q->wprep
-static int module_geo(const cimq_conv_desc* d, const cimq_lsq_desc* q, Geo* g, LsqArgs* la) {
+// the checks every module entry point shares; applies q->wprep.  shift: the cimq_module_shift_*
+// entry points (the shift ADC on the fast path, no prepared weight side)
+static int module_geo(const cimq_conv_desc* d, const cimq_lsq_desc* q, Geo* g, LsqArgs* la, bool shift = false) {
   CIMQ_TRY(make_geo(d, g));
   if (g->input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
-  if (g->variant == VAR_SHIFT_ROUND || g->variant == VAR_SHIFT_SIGN)
+  if (shift) {
+    if (g->variant != VAR_SHIFT_ROUND || !v7_plan(*g).ok || !shift_stats_ok(*g))
+      return fail(CIMQ_EUNSUPPORTED, "cimq_module_shift_*: the shift ADC on a fast-path layer only "
+                                     "(adc_variant CIMQ_ADC_SHIFT_ROUND, adc 1.5, 2 or 3 equal slices, v7 shapes)");
+    if (q && q->wprep) return fail(CIMQ_EINVAL, "cimq_module_shift_*: no prepared weight side");
+  } else if (g->variant == VAR_SHIFT_ROUND || g->variant == VAR_SHIFT_SIGN) {
     return fail(CIMQ_EUNSUPPORTED, "the module entry points run the library / stochastic ADC only");
+  }
   CIMQ_TRY(lsq_args(*g, q, la));
   g->wbase = reinterpret_cast<const unsigned char*>(q->wprep);
   return CIMQ_OK;
 }
 
-int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
-                        const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
-                        const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
-                        void* stream) {
+static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                               const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                               const float* beta_cim, const int8_t* binary_mask, const float* signed_act, float* out,
+                               void* ctx, void* ws, void* stream) {
   Geo g;
   LsqArgs la;
-  CIMQ_TRY(module_geo(d, q, &g, &la));
+  CIMQ_TRY(module_geo(d, q, &g, &la, beta_cim != nullptr));
   if (!x || !weight || !alpha_act || !alpha_weight || !binary_mask || !signed_act || !out || !ctx || !ws)
     return fail(CIMQ_EINVAL, "null pointer argument");
   const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
@@ -466,8 +474,13 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   float* scal = reinterpret_cast<float*>(wreg(g, c) + L.lsq_scal);
   {
     int nwblk;
-    const ModulePrep a = module_prep_args(g, x, weight, alpha_act, alpha_weight, has_alpha ? alpha_cim : nullptr,
-                                          binary_mask, signed_act, c, &nwblk);
+    ModulePrep a = module_prep_args(g, x, weight, alpha_act, alpha_weight, has_alpha ? alpha_cim : nullptr,
+                                    binary_mask, signed_act, c, &nwblk);
+    if (beta_cim) {  // the shift ADC: beta into the thresholds, and the per-channel beta sums
+      a.beta = beta_cim;
+      a.npp += g.Opad;
+      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
+    }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     ModulePrep aw = a;
@@ -494,6 +507,30 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
   hipLaunchKernelGGL(bpo_to_nchw_kernel, dim3(std::min(cdiv((long long)g.M * g.O, 256), 8192)), dim3(256), 0, s,
                      g, bpo, out);
   return check_hip("bpo_to_nchw");
+}
+
+int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                        const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                        const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
+                        void* stream) {
+  return module_forward_impl(d, q, x, weight, alpha_act, alpha_weight, alpha_cim, nullptr, binary_mask, signed_act,
+                             out, ctx, ws, stream);
+}
+
+int cimq_module_shift_supported(const cimq_conv_desc* d) {
+  Geo g;
+  if (make_geo(d, &g) != CIMQ_OK) return 0;
+  return (g.input_kind == CIMQ_INPUT_RAW_LSQ && g.variant == VAR_SHIFT_ROUND && v7_plan(g).ok && shift_stats_ok(g))
+             ? 1 : 0;
+}
+
+int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                              const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                              const float* beta_cim, const int8_t* binary_mask, const float* signed_act, float* out,
+                              void* ctx, void* ws, void* stream) {
+  if (!beta_cim || !alpha_cim) return fail(CIMQ_EINVAL, "cimq_module_shift_forward needs alpha_cim and beta_cim");
+  return module_forward_impl(d, q, x, weight, alpha_act, alpha_weight, alpha_cim, beta_cim, binary_mask, signed_act,
+                             out, ctx, ws, stream);
 }
 
 static int pending_run(Pending* pd, hipStream_t s) {
@@ -630,6 +667,40 @@ int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, c
   return module_tail(g, la, q, reinterpret_cast<const uint8_t*>(ctx), reinterpret_cast<uint8_t*>(ws), weight,
                      alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim,
                      reinterpret_cast<hipStream_t>(stream));
+}
+
+int cimq_module_shift_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                               const float* x, const float* weight, const float* alpha_act,
+                               const float* alpha_weight, const float* alpha_cim, const float* beta_cim,
+                               const int8_t* binary_mask, const float* signed_act, const void* ctx, float* grad_x,
+                               float* grad_weight, float* grad_alpha_act, float* grad_alpha_weight,
+                               float* grad_alpha_cim, float* grad_beta_cim, void* ws, void* stream) {
+  Geo g;
+  LsqArgs la;
+  CIMQ_TRY(module_geo(d, q, &g, &la, true));
+  (void)alpha_act; (void)alpha_weight; (void)beta_cim;
+  if (!grad_out || !x || !weight || !alpha_cim || !binary_mask || !signed_act || !ctx || !grad_x || !grad_weight ||
+      !grad_alpha_act || !grad_alpha_weight || !grad_alpha_cim || !grad_beta_cim || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  if (la.nbits_alpha == 0) return fail(CIMQ_EINVAL, "the shift ADC needs alpha_cim (nbits_alpha > 0)");
+  if (q->flags & CIMQ_LSQ_SKIP_TAIL) return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL with cimq_module_shift_backward");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  const float* scal = reinterpret_cast<const float*>(wreg(g, c) + L.lsq_scal);
+  g.onchw = 1;
+  bool lsq_fused = false;
+  CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
+  if (!lsq_fused || g.B * v7_plan(g).v.nbands != act_parts(g))
+    return fail(CIMQ_EINVAL, "internal: act-LSQ partials off the fused grad_x");
+  // d loss / d alpha_q and grad_beta (scale_shift.py:488-501) from the statistics kernel, then the
+  // module epilogue (grad_w + weight-LSQ backward, alpha_cim's quantiser, the step sizes) from there
+  CIMQ_TRY(launch_shift_stats(g, c, scal + 1, scal, grad_out, binary_mask, w, reinterpret_cast<float*>(w + W.gaq),
+                              grad_beta_cim, s, (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0));
+  return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                     grad_alpha_cim, s, 1);
 }
 
 int cimq_module_prepare(int n, const cimq_prepare_item* items, void* stream) {

@@ -634,7 +634,8 @@ inline bool shift_stats_ok(const Geo& g) {
   return shift_fast(g) && g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
 }
 int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
-                       const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s);
+                       const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s,
+                       int accum_beta = 0);
 int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
                      hipStream_t s);
 // cimq_part_bwd.hip: backward of layers outside the v7 plan (v5 / v6 and general kernels)

@@ -26,6 +26,7 @@ struct ModulePrep {
   const float* alpha_cim;
   const float* signed_act;
   const int8_t* bmask;
+  const float* beta;  // beta_cim of the shift ADC module entry points (null otherwise)
   uint8_t* xcf;
   uint8_t* xcb;
   v4i* wfrag;
@@ -119,6 +120,8 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
         }
       }
     }
+    if (a.beta)  // the shift ADC's thresholds need a finite beta everywhere (params_item)
+      for (int e = threadIdx.x; e < q.nalpha; e += blockDim.x) lit = lit || !isfinite(a.beta[e]);
     lit = __syncthreads_or(lit);
     if (threadIdx.x == 0) {
       a.scal[0] = sa;
@@ -136,7 +139,7 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wtc_item(g, ws, a.Cp, a.wtc, t - e2);
     else if (t < e4) wcy_item(g, ws, a.ncpbt, a.wcy, t - e3);
-    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4);
+    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4, a.beta);
   }
 }
 

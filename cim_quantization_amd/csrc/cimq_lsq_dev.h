@@ -87,6 +87,7 @@ struct ModuleTail {
   float* gapart;  // wide alpha_cim (> kFinishInReg elements): [nga][4] first-sweep partials, else null
   float cgrad;    // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
   int nchunks, nwb, nga, napart, accum;
+  int gaq_ready;  // d loss / d alpha_q already in gaq (the shift ADC's statistics kernel): no slab sums
 };
 // alpha_cim sizes the one-block epilogue keeps in registers (module_finish_block); larger ones
 // (the QuantLinear layers: T * nbw * nba * O = 131072 at 1024 -> 1024 w4a4) take the wide path:
@@ -142,7 +143,7 @@ __device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleT
   const int nkj = g.nbw * g.nba;
   const size_t nout = (size_t)g.T * nkj * g.Opad;
   const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
-  const float s = reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+  const float s = a.gaq_ready ? 0.f : reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
   if ((threadIdx.x >> 6) != 0) return;
   float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
   if (idx < nout) {
@@ -153,8 +154,13 @@ __device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleT
       const int i = (int)(qq / nkj);
       const int k = kj / g.nba, j = kj - k * g.nba;
       const size_t e = (((size_t)i * g.nbw + k) * g.nba + j) * g.O + o;
-      const float G = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
-      a.gaq[e] = G;
+      float G;
+      if (a.gaq_ready) {
+        G = a.gaq[e];
+      } else {
+        G = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
+        a.gaq[e] = G;
+      }
       if (a.gapart) {  // alpha_cim_bwd_block's first sweep, this element
         const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
         const float qp_al = (float)((1 << q.nbits_alpha) - 1);

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void shift_stats_kernel(Geo g, V3 v, const uin
 __global__ __launch_bounds__(256) void shift_combine_kernel(Geo g, const float* __restrict__ slab, int nsc,
                                                             const int8_t* __restrict__ bmask,
                                                             float* __restrict__ grad_alpha,
-                                                            float* __restrict__ grad_beta) {
+                                                            float* __restrict__ grad_beta, int accum_beta) {
   const int nkj = g.nbw * g.nba;
   const int total = g.T * nkj * g.O;
   const int lane = threadIdx.x & 63;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void shift_combine_kernel(Geo g, const float* 
     if (lane == 0) {
       const float mk = (float)bmask[kj];  // binary_mask[0, 0, k, j, 0, 0]
       grad_alpha[t] = a * mk;
-      grad_beta[t] = c * mk;
+      grad_beta[t] = accum_beta ? grad_beta[t] + c * mk : c * mk;  // torch's AccumulateGrad when asked
     }
   }
 }
@@ -213,7 +213,8 @@ inline bool shift_table_fits(const Geo& g) {
 }
 
 int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
-                       const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s) {
+                       const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s,
+                       int accum_beta) {
   const Plan3 p = v3_plan(g);
   if (!p.ok || !shift_stats_ok(g)) return fail(CIMQ_EUNSUPPORTED, "internal: shift statistics off the fast path");
   CtxLayout L = ctx_layout(g);
@@ -250,7 +251,7 @@ int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const 
   CIMQ_TRY(check_hip("shift_stats"));
   const int total = g.T * nkj * g.O;
   hipLaunchKernelGGL(shift_combine_kernel, dim3(std::min(cdiv(total, 4), 2048)), dim3(256), 0, s, g, slab, nsc,
-                     bmask, grad_alpha, grad_beta);
+                     bmask, grad_alpha, grad_beta, accum_beta);
   return check_hip("shift_combine");
 }
 

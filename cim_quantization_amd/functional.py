@@ -629,6 +629,95 @@ def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, 
                                 nbits_alpha, accumulate, stochastic, tail_stream, wprep)
 
 
+def _shift_module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, xbar,
+                        nbits_alpha):
+    desc, lsq = _module_descs(tuple(x_shape), weight, stride, padding, dilation, nbits_a, abitslice, nbits_w,
+                              wbitslice, 1.5, xbar, nbits_alpha, True, False)
+    desc.adc_variant = _lib.CIMQ_ADC_SHIFT_ROUND
+    return desc, lsq
+
+
+def module_shift_supported(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice,
+                           adcbits, xbar, nbits_alpha):
+    """Whether cim_module_shift_conv takes this Conv2dLSQCiM(adc_shift=True) layer (libcimq's fused
+    shift path: adc 1.5, 2 or 3 equal slices, a fast-path conv shape); else the module quantises in
+    torch and calls the unfused shift entry points."""
+    if adcbits != 1.5 or len(x_shape) != 4:
+        return False
+    dl = tuple(dilation) if isinstance(dilation, (tuple, list)) else (dilation, dilation)
+    if dl != (1, 1):
+        return False
+    desc, _ = _shift_module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice,
+                                  xbar, nbits_alpha)
+    return bool(_lib.load().cimq_module_shift_supported(desc))
+
+
+class _CimModuleShiftConv(torch.autograd.Function):
+    """Conv2dLSQCiM(adc_shift=True) after its first-step init: as _CimModuleConv (activation, weight and
+    alpha_cim quantisers inside libcimq), with the scale + shift ADC of test_backward_cimlayer_scale_
+    shift.py:336-546 on the rescaled partial sum; differentiable in x, weight, alpha_act, alpha_weight,
+    alpha_cim and beta_cim.  NCHW output."""
+
+    @staticmethod
+    def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, beta_cim, binary_mask, signed_act, stride,
+                padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, xbar, nbits_alpha):
+        _require_device(x)
+        dev = x.device
+        B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
+        desc, lsq = _shift_module_descs(tuple(x.shape), weight, st, pd, dilation, nbits_a, abitslice, nbits_w,
+                                        wbitslice, xbar, nbits_alpha)
+        sizes = _lib.query_sizes(desc)
+        xc = x.detach().to(torch.float32).contiguous()
+        wc = weight.detach().to(torch.float32).contiguous()
+        aa = alpha_act.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        aw = alpha_weight.detach().to(torch.float32).reshape(-1)[:1].contiguous()
+        ac = alpha_cim.detach().to(torch.float32).contiguous()
+        bc = beta_cim.detach().to(torch.float32).contiguous()
+        bm = binary_mask.to(device=dev, dtype=torch.int8).contiguous()
+        sg = signed_act.detach().to(device=dev, dtype=torch.float32).reshape(-1)[:1].contiguous()
+        Ho = (H + 2 * pd[0] - KH) // st[0] + 1
+        Wo = (W + 2 * pd[1] - KW) // st[1] + 1
+        out = torch.empty(B, O, Ho, Wo, device=dev, dtype=torch.float32)
+        cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+        ws = torch.empty(max(sizes.fwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        _lib.check(_lib.load().cimq_module_shift_forward(desc, lsq, xc.data_ptr(), wc.data_ptr(), aa.data_ptr(),
+                                                         aw.data_ptr(), ac.data_ptr(), bc.data_ptr(), bm.data_ptr(),
+                                                         sg.data_ptr(), out.data_ptr(), cbuf.data_ptr(),
+                                                         ws.data_ptr(), _stream()), "cimq_module_shift_forward")
+        ctx.desc, ctx.lsq, ctx.sizes = desc, lsq, sizes
+        ctx.bufs = (xc, wc, aa, aw, ac, bc, bm, sg, cbuf)
+        ctx.save_for_backward(x, weight, alpha_act, alpha_weight, alpha_cim, beta_cim)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        ctx.saved_tensors  # noqa: B018 -- version check of x and the parameters
+        xc, wc, aa, aw, ac, bc, bm, sg, cbuf = ctx.bufs
+        dev = xc.device
+        g = grad_output.detach().to(torch.float32).contiguous()
+        gx = torch.empty_like(xc)
+        gw = torch.empty_like(wc)
+        gaa = torch.empty(1, device=dev, dtype=torch.float32)
+        gaw = torch.empty(1, device=dev, dtype=torch.float32)
+        gac = torch.empty_like(ac)
+        gbc = torch.empty_like(bc)
+        ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
+        _lib.check(_lib.load().cimq_module_shift_backward(
+            ctx.desc, ctx.lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(), aa.data_ptr(), aw.data_ptr(), ac.data_ptr(),
+            bc.data_ptr(), bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(), gw.data_ptr(), gaa.data_ptr(),
+            gaw.data_ptr(), gac.data_ptr(), gbc.data_ptr(), ws.data_ptr(), _stream()), "cimq_module_shift_backward")
+        return (gx, gw, gaa, gaw, gac, gbc) + (None,) * 11
+
+
+def cim_module_shift_conv(x, weight, alpha_act, alpha_weight, alpha_cim, beta_cim, binary_mask, signed_act, stride,
+                          padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, xbar, nbits_alpha):
+    """NCHW output of a Conv2dLSQCiM(adc_shift=True, adcbits=1.5) layer with its quantisers fused
+    (module_shift_supported must hold)."""
+    return _CimModuleShiftConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, beta_cim, binary_mask,
+                                     signed_act, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice,
+                                     xbar, nbits_alpha)
+
+
 def alpha_cim_init(x, w_q, sa, sw, binary_mask, signed_act, stride, padding, nbits_a, abitslice,
                    nbits_w, wbitslice, adcbits, xbar, num_xbars):
     """First-step alpha_cim initialisation on the device (lsq.py:557-563, 35-87)."""

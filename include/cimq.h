@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 7
+#define CIMQ_ABI_VERSION 8
 
 /* status codes */
 #define CIMQ_OK 0
@@ -174,6 +174,28 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
 int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
                               const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
                               float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
+
+/* cimq_module_forward / cimq_module_backward for Conv2dLSQCiM(adc_shift=True): the per-tile scale +
+ * shift ADC clamp(round((u - beta) / alpha_q), -1, 1) * alpha_q + beta of
+ * test/test_backward_cimlayer_scale_shift.py:336-546 applied to the library's rescaled partial sum
+ * u = fp16(ps) * sw * sa, with the three quantisers inside the library as for the library ADC.
+ * Requires adc_variant = CIMQ_ADC_SHIFT_ROUND (no flags), adc_bits 1.5, input_kind =
+ * CIMQ_INPUT_RAW_LSQ, nbw = nba = 2 or 3 and a layer the fast path takes (3x3, pad 1, stride 1 or 2,
+ * power-of-two output width and channels); CIMQ_EUNSUPPORTED otherwise (the caller then quantises
+ * in torch and calls cimq_shift_forward / cimq_shift_backward).  No prepared weight side
+ * (q->wprep NULL), no CIMQ_LSQ_SKIP_TAIL.  beta_cim / grad_beta_cim: [1, T, nbw, nba, 1, O] like
+ * alpha_cim; CIMQ_LSQ_ACCUMULATE_GRADS adds into grad_beta_cim as well.  Since ABI 8. */
+int cimq_module_shift_supported(const cimq_conv_desc* d); /* 1 if the two calls below take d, else 0 */
+int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
+                              const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
+                              const float* beta_cim, const int8_t* binary_mask, const float* signed_act, float* out,
+                              void* ctx, void* ws, void* stream);
+int cimq_module_shift_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                               const float* x, const float* weight, const float* alpha_act,
+                               const float* alpha_weight, const float* alpha_cim, const float* beta_cim,
+                               const int8_t* binary_mask, const float* signed_act, const void* ctx, float* grad_x,
+                               float* grad_weight, float* grad_alpha_act, float* grad_alpha_weight,
+                               float* grad_alpha_cim, float* grad_beta_cim, void* ws, void* stream);
 
 /* One layer of cimq_module_prepare: its descriptors (as the forward will receive them; the
  * lsq descriptor's wprep and flags are ignored here) and raw parameters, and its output buffer
