@@ -132,3 +132,23 @@ def test_module_prepare_validates_items(lib):
     assert lib.cimq_module_prepare(-1, None, None) == 1
     assert lib.cimq_module_prepare(0, None, None) == 0
     assert L.query_sizes(d).wprep_bytes > 0
+
+
+@pytest.mark.parametrize("C,O,H,s", [(16, 16, 32, 1), (32, 32, 16, 1), (64, 64, 8, 1), (16, 32, 32, 2),
+                                     (32, 64, 16, 2)])
+def test_module_shift_supported_resnet56_shapes(lib, C, O, H, s):
+    """cfg4's Conv2dLSQCiM(adc_shift=True) layers (w2a2 xbar 64, adc 1.5) take the fused shift path;
+    the test scripts' variants (int8 ps buffer, shift range), the sign ADC, the w8a8 first layer and
+    non-RAW input do not (host plan only, no GPU call)."""
+    kw = dict(B=256, C=C, H=H, W=H, O=O, stride=(s, s), xbar=64, bits_w=2, bits_a=2,
+              input_kind=L.CIMQ_INPUT_RAW_LSQ, lsq_qp=3.0)
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw)) == 1
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_LIBRARY, **kw)) == 0
+    scripts = L.CIMQ_ADC_SHIFT_ROUND | L.CIMQ_ADC_F_PS_INT8 | L.CIMQ_ADC_F_SHIFT_RANGE
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=scripts, **kw)) == 0
+    kw1 = dict(kw, adc_bits=1.0)
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_SIGN, **kw1)) == 0
+    kw8 = dict(kw, C=3, O=16, H=32, W=32, stride=(1, 1), bits_w=8, bits_a=8, lsq_qp=255.0)
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw8)) == 0
+    kwx = dict(kw, input_kind=L.CIMQ_INPUT_XQ)
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kwx)) == 0
