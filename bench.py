@@ -39,7 +39,7 @@ XBAR, ADC = 128, 1.5
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward runs bf16 x3
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
-TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r02_final", "pmc_traffic.json"))
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r03_final", "pmc_traffic.json"))
 # rocprof symbol of each v7-path kernel id (the names pmc_traffic.json is keyed by)
 V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, 3, ", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
               "gw_v7": "cimq::cim_bwd_gw_v7_kernel<3, 3>"}
