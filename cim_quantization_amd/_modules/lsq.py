@@ -170,7 +170,29 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         return out
 
 
-class Conv2dLSQ(_Conv2dQ):
+class _HostFlags:
+    """Host mirror of the init_state (and ActLSQ's signed) buffers for the plain modules.
+
+    The reference tests ``self.init_state == 0`` (and ActLSQ ``self.signed == 1``) on every
+    forward (lsq.py:404, :641, :611); on a GPU tensor each test is a device sync that stalls the
+    launch queue. The values are read once and cached. The cache is reset by load_state_dict
+    and by dist.GradBucket.broadcast_from; code that writes the buffers directly sets
+    ``_state_cache = None``, as for Conv2dLSQCiM."""
+
+    _state_cache = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._state_cache = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    def _flags(self):
+        if self._state_cache is None:
+            sg = getattr(self, "signed", None)
+            self._state_cache = [bool(self.init_state.item() != 0), sg is not None and bool(sg.item() == 1)]
+        return self._state_cache
+
+
+class Conv2dLSQ(_HostFlags, _Conv2dQ):
     """Plain LSQ conv (lsq.py:389-436); consumes the (x_q, act_scale) tuple of ActLSQ.
 
     The weight quantiser runs on libcimq (lsq_quantize) and the conv of the two integer-code
@@ -189,9 +211,10 @@ class Conv2dLSQ(_Conv2dQ):
             return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
         x_q, act_scale = x
         qn, qp = _weight_range(self.nbits)
-        if self.training and self.init_state == 0:
+        if self.training and not self._flags()[0]:
             self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
             self.init_state.fill_(1)
+            self._flags()[0] = True
         ws = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
         w_q = lsq_quantize(self.weight, ws, qn, qp)
         code_range = getattr(x_q, "_cimq_code_range", None)
@@ -202,7 +225,7 @@ class Conv2dLSQ(_Conv2dQ):
         return y * act_scale * ws
 
 
-class LinearLSQ(_LinearQ):
+class LinearLSQ(_HostFlags, _LinearQ):
     """Plain LSQ linear (lsq.py:591-617): the weight quantiser on libcimq, the fp32 linear of the
     unquantised input by torch's GEMM (the reference quantises only the weight here)."""
 
@@ -213,14 +236,15 @@ class LinearLSQ(_LinearQ):
         if self.alpha is None:
             return F.linear(x, self.weight, self.bias)
         qn, qp = _weight_range(self.nbits)
-        if self.training and self.init_state == 0:
+        if self.training and not self._flags()[0]:
             self.alpha.data.copy_(2 * self.weight.abs().mean() / math.sqrt(qp))
             self.init_state.fill_(1)
+            self._flags()[0] = True
         a = grad_scale(self.alpha, 1.0 / math.sqrt(self.weight.numel() * qp))
         return F.linear(x, lsq_quantize(self.weight, a, qn, qp, scaled=True), self.bias)
 
 
-class ActLSQ(_ActQ):
+class ActLSQ(_HostFlags, _ActQ):
     """LSQ activation quantiser (lsq.py:620-662): returns (integer codes, step size); the codes
     come from libcimq and carry their range for Conv2dLSQ's int8 conv."""
 
@@ -228,19 +252,21 @@ class ActLSQ(_ActQ):
         super().__init__(nbits=nbits_a)
 
     def _range(self):
-        if self.signed == 1:
+        if self._flags()[1]:
             return -(2 ** (self.nbits - 1)), 2 ** (self.nbits - 1) - 1
         return 0, 2 ** self.nbits - 1
 
     def forward(self, x):
         if self.alpha is None:
             return x
-        if self.training and self.init_state == 0:
+        if self.training and not self._flags()[0]:
             if x.min() < -1e-5:
                 self.signed.data.fill_(1)
+                self._flags()[1] = True
             _, qp = self._range()
             self.alpha.data.copy_(2 * x.abs().mean() / math.sqrt(qp))
             self.init_state.fill_(1)
+            self._flags()[0] = True
         qn, qp = self._range()
         a = grad_scale(self.alpha, 1.0 / math.sqrt(x.numel() * qp))
         x_q = lsq_quantize(x, a, qn, qp)

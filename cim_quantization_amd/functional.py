@@ -820,6 +820,9 @@ def num_xbars(in_channels, kernel_size, xbar) -> int:
 # =============================================================================================
 # plain LSQ modules (lsq.py:389-436 Conv2dLSQ, :591-617 LinearLSQ, :620-662 ActLSQ)
 # =============================================================================================
+_LSQ_WS = {}  # cimq_lsq_quantize_workspace_bytes per element count
+
+
 class _LsqQuantize(torch.autograd.Function):
     """out = round_pass(clamp(x / s, qn, qp)) [* s] with s the grad-scaled step size (a [1]
     tensor: grad_scale(alpha, g) evaluated by torch, so its graph back to alpha stays torch's).
@@ -847,8 +850,11 @@ class _LsqQuantize(torch.autograd.Function):
         gc = g.float().contiguous()
         gx = torch.empty_like(xc)
         gs = torch.empty(1, device=xc.device, dtype=torch.float32)
-        ws = torch.empty(max(lib.cimq_lsq_quantize_workspace_bytes(xc.numel()), 4), device=xc.device,
-                         dtype=torch.uint8)
+        n = xc.numel()
+        nb = _LSQ_WS.get(n)
+        if nb is None:
+            nb = _LSQ_WS[n] = max(lib.cimq_lsq_quantize_workspace_bytes(n), 4)
+        ws = torch.empty(nb, device=xc.device, dtype=torch.uint8)
         _lib.check(lib.cimq_lsq_quantize_backward(xc.data_ptr(), xc.numel(), sc.data_ptr(), qn, qp, scaled,
                                                   gc.data_ptr(), gx.data_ptr(), gs.data_ptr(), ws.data_ptr(),
                                                   _stream()), "cimq_lsq_quantize_backward")
@@ -858,6 +864,21 @@ class _LsqQuantize(torch.autograd.Function):
 def lsq_quantize(x, s, qn, qp, scaled=False):
     """LSQ fake-quantiser on libcimq: round_pass(clamp(x / s, qn, qp)) [* s] (lsq.py:412,611,656)."""
     return _LsqQuantize.apply(x, s, qn, qp, scaled)
+
+
+_QCONV_PLANS = {}
+
+
+def _qconv_plan(*key):
+    """descriptor and workspace sizes of one conv shape, built once (host time per call)"""
+    p = _QCONV_PLANS.get(key)
+    if p is None:
+        B, C, H, W, O, KH, KW, stride, padding, dilation, code_range, has_bias = key
+        desc = _lib.make_qconv_desc(B, C, H, W, O, KH, KW, stride, padding, dilation, 1, code_range[0],
+                                    code_range[1], has_bias)
+        p = (desc,) + tuple(_lib.qconv_sizes(desc))
+        _QCONV_PLANS[key] = p
+    return p
 
 
 class _QConv2d(torch.autograd.Function):
@@ -876,9 +897,7 @@ class _QConv2d(torch.autograd.Function):
         bc = None if bias is None else bias.detach().float().contiguous()
         B, C, H, W = xc.shape
         O, _, KH, KW = wc.shape
-        desc = _lib.make_qconv_desc(B, C, H, W, O, KH, KW, stride, padding, dilation, 1, code_range[0],
-                                    code_range[1], bc is not None)
-        fws, bws = _lib.qconv_sizes(desc)
+        desc, fws, bws = _qconv_plan(B, C, H, W, O, KH, KW, stride, padding, dilation, code_range, bc is not None)
         Ho = (H + 2 * padding[0] - dilation[0] * (KH - 1) - 1) // stride[0] + 1
         Wo = (W + 2 * padding[1] - dilation[1] * (KW - 1) - 1) // stride[1] + 1
         y = torch.empty(B, O, Ho, Wo, device=xc.device, dtype=torch.float32)
