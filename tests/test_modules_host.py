@@ -65,3 +65,22 @@ def test_grad_scale_and_round_pass_values():
     assert r.tolist() == [0.0, 2.0, 2.0, -0.0, 2.0]
     r.sum().backward()
     assert v.grad.tolist() == [1.0] * 5
+
+
+def test_plain_modules_host_flag_mirror():
+    """Conv2dLSQ / ActLSQ read init_state / signed once (no device sync per forward); a
+    load_state_dict and GradBucket.broadcast_from reset the mirror."""
+    from cim_quantization_amd._modules.lsq import ActLSQ, Conv2dLSQ
+    act, conv = ActLSQ(nbits_a=4), Conv2dLSQ(4, 4, 3, nbits_w=4)
+    assert act._flags() == [False, False] and conv._flags() == [False, False]
+    sd = act.state_dict()
+    sd["init_state"].fill_(1)
+    sd["signed"].fill_(1)
+    act.load_state_dict(sd)
+    assert act._flags() == [True, True]
+    assert act._range() == (-8, 7)
+    with torch.no_grad():
+        conv.init_state.fill_(1)
+    assert conv._flags()[0] is False  # a direct buffer write needs the reset, as for Conv2dLSQCiM
+    conv._state_cache = None
+    assert conv._flags()[0] is True
