@@ -174,7 +174,7 @@ class _HostFlags:
     """Host mirror of the init_state (and ActLSQ's signed) buffers for the plain modules.
 
     The reference tests ``self.init_state == 0`` (and ActLSQ ``self.signed == 1``) on every
-    forward (lsq.py:404, :641, :611); on a GPU tensor each test is a device sync that stalls the
+    forward (lsq.py:407, :601, :628, :634, :643); on a GPU tensor each test is a device sync that stalls the
     launch queue. The values are read once and cached. The cache is reset by load_state_dict
     and by dist.GradBucket.broadcast_from; code that writes the buffers directly sets
     ``_state_cache = None``, as for Conv2dLSQCiM."""
