@@ -34,13 +34,10 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
     const Plan7 p7 = v7_plan(g);
     // the general / v6 grad_x operands only where the v7 backward will not run
     if (!(p7.ok && (g.variant == VAR_LIBRARY || shift_stats_ok(g)))) {
+      // the general grad_x operand where the v7 backward will not run
       int total = g.T * g.FBT * g.NKS * 64;
       hipLaunchKernelGGL(prep_wgx_kernel, dim3(cdiv(total, blk)), dim3(blk), 0, s, g, w_q, sw,
                          reinterpret_cast<v4i*>(wreg(g, ctx) + L.wgx));
-      const int Cp = (g.C + 15) / 16 * 16;
-      const int tw = g.T * g.KHW * Cp * g.NKS * 4;
-      hipLaunchKernelGGL(prep_wtc_kernel, dim3(cdiv(tw, blk)), dim3(blk), 0, s, g, w_q, sw, Cp,
-                         reinterpret_cast<uint4*>(wreg(g, ctx) + L.wtc));
       CIMQ_TRY(check_hip("prep_wgx"));
     }
     if (p7.ok) {
@@ -289,8 +286,7 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
     float* part = reinterpret_cast<float*>(w + W.lsq_part);
     int nparts;
     if (lsq_fused) {
-      const Plan7 p7 = v7_plan(g);
-      nparts = g.B * (p7.ok ? p7.v.nbands : v3_plan(g).v.nbands);
+      nparts = g.B * v7_plan(g).v.nbands;
     } else {
       int grid = cdiv(g.Nin, 256);
       if (grid > kLsqParts) grid = kLsqParts;
@@ -304,13 +300,11 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   return CIMQ_OK;
 }
 
-// number of act-LSQ partials the backward leaves in ws (fused into the fast grad_x kernels, else
+// number of act-LSQ partials the backward leaves in ws (fused into the v7 grad_x kernel, else
 // one per lsq_act_bwd_kernel block)
 static int act_parts(const Geo& g) {
   const Plan7 p7 = v7_plan(g);
   if (p7.ok) return g.B * p7.v.nbands;
-  const Plan3 p3 = v3_plan(g);
-  if (p3.ok) return g.B * p3.v.nbands;
   int grid = cdiv(g.Nin, 256);
   return grid > kLsqParts ? kLsqParts : grid;
 }
@@ -407,7 +401,6 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
                                    const float* signed_act, uint8_t* c, int* nwblk) {
   CtxLayout L = ctx_layout(g);
   uint8_t* wr = wreg(g, c);
-  const bool fast = v3_plan(g).ok;
   const Plan7 p7 = v7_plan(g);
   ModulePrep a;
   memset(&a, 0, sizeof(a));
@@ -422,19 +415,16 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
   a.xcb = c ? c + L.xhat : nullptr;
   a.wfrag = reinterpret_cast<v4i*>(wr + L.wfrag);
   a.wgx = reinterpret_cast<v4i*>(wr + L.wgx);
-  a.wtc = reinterpret_cast<uint4*>(wr + L.wtc);
   a.wcy = reinterpret_cast<v4i*>(wr + L.wcy);
-  a.Cp = (g.C + 15) / 16 * 16;
   a.pp = params_of(g, c);
   a.scal = reinterpret_cast<float*>(wr + L.lsq_scal);
   a.nact_blocks = (int)std::min<long long>(cdiv(g.Nin, 4 * 256), act_blocks());
   a.nwf = g.T * g.KS * g.NBLK * 64;
-  a.nwg = fast ? 0 : g.T * g.FBT * g.NKS * 64;                   // general grad_x operand
-  a.nwt = (fast && !p7.ok) ? g.T * g.KHW * a.Cp * g.NKS * 4 : 0;  // v5 / v6 grad_x operand
+  a.nwg = p7.ok ? 0 : g.T * g.FBT * g.NKS * 64;       // general / dense grad_x operand
   a.ncpbt = p7.ok ? p7.v.NCPBT : 1;
-  a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;              // v8 grad_x operand
+  a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;  // v8 grad_x operand
   a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
+  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.npp, 256), 1024));
   return a;
 }
 
@@ -479,7 +469,7 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
     if (beta_cim) {  // the shift ADC: beta into the thresholds, and the per-channel beta sums
       a.beta = beta_cim;
       a.npp += g.Opad;
-      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwt + a.nwc + a.npp, 256), 1024));
+      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.npp, 256), 1024));
     }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     const int slot = prof_begin(KID_PREP_ACT, g, s);
@@ -594,8 +584,7 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
   if (lsq_fused) {
-    const Plan7 p7 = v7_plan(g);
-    nparts = g.B * (p7.ok ? p7.v.nbands : p.v.nbands);
+    nparts = g.B * v7_plan(g).v.nbands;
   } else {
     int grid = cdiv(g.Nin, 256);
     if (grid > kLsqParts) grid = kLsqParts;

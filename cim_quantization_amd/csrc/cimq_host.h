@@ -154,7 +154,7 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wtc, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
@@ -166,7 +166,6 @@ inline CtxLayout ctx_layout(const Geo& g) {
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
-  L.wtc = o; o = align256(o + (size_t)g.T * g.KHW * ((g.C + 15) / 16 * 16) * g.NKS * 32 * 2);
   L.wcy = o; o = align256(o + (size_t)g.T * 12 * g.NKS * 64 * 16);  // v8 grad_x operand (<= 12 blocks / tile)
   L.thi = o; o = align256(o + npar * 4);
   L.tlo = o; o = align256(o + npar * 4);
@@ -232,20 +231,19 @@ const int kLsqParts = 1024;
 inline size_t lds_tile(const Geo& g) {
   return align256((size_t)g.nba * 64 * g.KTP + 2 * sizeof(int) * g.KS * 64 + sizeof(int4) * 64);
 }
+// general grad_w: the tile, per-wave code * g and beta-term sums [2][4 waves][nkj][32], the grad_w
+// block sum, the backward slices
 inline size_t lds_gw(const Geo& g) {
-  return lds_tile(g) + 2 * sizeof(float) * g.nbw * g.nba * 32 + sizeof(float) * g.FBT * 16 * 32 +
+  return lds_tile(g) + 2 * 4 * sizeof(float) * g.nbw * g.nba * 32 + sizeof(float) * g.FBT * 16 * 32 +
          (size_t)g.nba * g.KS * 64 * 64;
 }
 const size_t kLdsMax = 160 * 1024;
-
-inline bool gx_lds_ok(const Geo& g) { return lds_tile(g) + sizeof(float) * g.C * g.HW <= kLdsMax - 1024; }
 
 // ---- v3 fast path (whole-row 64-pixel tiles): patch geometry and LDS budgets ----
 struct Plan3 {
   bool ok;
   V3 v;
-  size_t lds_fwd, lds_gx, lds_gw, lds_init;
-  size_t lds_gx6;  // 0: cim_bwd_gx_v6_kernel does not apply
+  size_t lds_fwd;
 };
 
 inline size_t a16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -292,42 +290,14 @@ inline Plan3 v3_plan(const Geo& g) {
   const size_t patch = a16((size_t)g.C * v.RH * v.WP * g.NBP);
   v.obm = tune("FWD_OBM", 2);  // two o-blocks per block (measured best for O = 32 / 64)
   if (v.obm != 1 && v.obm != 2 && v.obm != 4) v.obm = 4;
-  const int nof = std::min(v.obm, g.OB16), nog = std::min(2, g.OB16);
+  const int nof = std::min(v.obm, g.OB16);
   const size_t fwd_common = patch + (size_t)g.T * g.KS * 64 * 4 + ckl;
   const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * (16 + 4);
   const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
   v.fwd_res = fwd_res <= (size_t)tune("FWD_RES_KB", 52) * 1024 ? 1 : 0;
   p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
-  p.lds_gx = a16((size_t)3 * (v.NPB + 1) * 32 * 2) + a16((size_t)g.KHW * v.CB * 16 * 40 * 2) + ckl + 64;
-  {
-    // v6: G rows at pitch 40, two W buffers of the tile's channel blocks, the band's grad_out
-    // slab, two state buffers
-    v.NCBT = 0;
-    for (int i = 0; i < g.T; ++i) {
-      const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
-      v.NCBT = std::max(v.NCBT, c1 / 16 - c0 / 16 + 1);
-    }
-    const size_t pq = (size_t)64 * (g.NBP == 4 ? 2 : 4);
-    const size_t l6 = a16((size_t)3 * (v.NPB + 1) * 40 * 2) + 2 * a16((size_t)g.KHW * v.NCBT * 16 * 64) +
-                      a16((size_t)g.O * v.NPB * 4) + 2 * a16((size_t)2 * (v.NPB / 4) * pq) + ckl + 64;
-    p.lds_gx6 = (g.O % 16 == 0 && l6 <= kLdsMax - 512) ? l6 : 0;
-#ifdef CIMQ_GX_V5
-    p.lds_gx6 = 0;
-#endif
-  }
-  v.NCG = 0;
-  for (int i = 0; i < g.T; ++i) {
-    const int c0 = (i * g.xbar) / g.KHW, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
-    v.NCG = std::max(v.NCG, c1 - c0 + 1);
-  }
-  const size_t pg = a16((size_t)v.NCG * v.RH * v.WP * g.NBP);
-  const size_t gw_tail = (size_t)g.KS * 64 * 4 + (size_t)g.nbw * nog * g.KS * 1024 + (size_t)nkj * nog * 16 * 16 +
-                         a16((size_t)nkj * 32 * 4 * 4) + ckl;  // init: per-wave |u| rows
-  p.lds_gw = std::max(a16(2 * (size_t)v.NCG * v.RH * v.WP * g.NBP), (size_t)g.FBT * 16 * 32 * 4) + 128 * 4 +
-             a16((size_t)nkj * 16 * 4) + ckl;
-  p.lds_init = pg + gw_tail;
   const size_t lim = kLdsMax - 512;
-  p.ok = p.lds_fwd <= lim && p.lds_gx <= lim && p.lds_gw <= lim;
+  p.ok = p.lds_fwd <= lim;
   return p;
 }
 
@@ -501,8 +471,23 @@ inline int dense_rows_per_chunk(const Geo& g) {
   return ((g.M + n - 1) / n + 31) / 32 * 32;
 }
 
+// the shift ADC's statistics kernel (cimq_part_shift.hip) applies: interleaved 3-bit state words of
+// w2a2 / w3a3 on a v7 shape (other shift layers take the general backward)
+inline bool shift_stats_ok(const Geo& g) {
+  return shift_fast(g) && g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
+}
+// half-range of its q tables: the largest |ps| of 0 .. 2^bs - 1 slices over one tile (the sign slice of
+// the weights included); larger partial sums (slice artifacts) take the direct evaluation
+inline int shift_table_range(const Geo& g) {
+  const int tmax = std::min(g.K, g.xbar);
+  return tmax * ((1 << g.bsa) - 1) * ((1 << g.bsw) - 1);
+}
+inline bool shift_table_fits(const Geo& g) {
+  return (size_t)g.nbw * g.nba * 16 * (2 * shift_table_range(g) + 1) * 4 <= 48 * 1024;
+}
+
 struct WsLayout {
-  size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, total;
+  size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
   int rows, nchunks, nchunks_bwd;
 };
 
@@ -526,11 +511,13 @@ inline WsLayout ws_layout(const Geo& g) {
   W.gb_slab = o; o = align256(o + (g.variant == VAR_SHIFT_ROUND || g.variant == VAR_SHIFT_SIGN
                                        ? sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad : 0));
   // shift ADC on the fast path: per pixel chunk, tile, pair and channel the grad_alpha / grad_beta partials
-  W.ss_slab = o; o = align256(o + (shift_fast(g) ? sizeof(float) * shift_chunks(g) * g.T * 2 * g.nbw * g.nba * g.Opad : 0));
-  // and its q tables [T][OB16][nbw * nba][16][2R + 1] (R = shift_table_range, <= 48 KB per block)
-  W.qtab = o; o = align256(o + (shift_fast(g) ? sizeof(float) * (size_t)g.T * g.OB16 * g.nbw * g.nba * 16 *
-                                                    (2 * std::min(g.K, g.xbar) * ((1 << g.bsa) - 1) * ((1 << g.bsw) - 1) + 1)
-                                              : 0));
+  // shift ADC statistics (v7 shapes, shift_stats_ok): per pixel chunk, tile, pair and channel the
+  // grad_alpha / grad_beta partials, and the q tables [T][OB16][nbw * nba][16][2R + 1] when they fit
+  const bool stats = p7.ok && shift_stats_ok(g);
+  W.ss_slab = o; o = align256(o + (stats ? sizeof(float) * shift_chunks(g) * g.T * 2 * g.nbw * g.nba * g.Opad : 0));
+  W.qtab = o; o = align256(o + ((stats && shift_table_fits(g)) ? sizeof(float) * (size_t)g.T * g.OB16 * g.nbw * g.nba *
+                                                                    16 * (2 * shift_table_range(g) + 1)
+                                                              : 0));
   W.lsq_part = o; o = align256(o + sizeof(float) * std::max(kLsqParts, g.B * g.H));  // >= B * bands
   // module entry points: d loss / d alpha_q, weight-LSQ partials of the grad_w reducer, and
   // a [B, P, O] staging copy of out / grad_out for the general kernels
@@ -538,6 +525,8 @@ inline WsLayout ws_layout(const Geo& g) {
   W.gapart = o; o = align256(o + sizeof(float) * 4 * (size_t)cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64));
   W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
   W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
+  // the general backward's unfolded grad_x [M][K] (folded by fold_gx_kernel)
+  W.gxu = o; o = align256(o + ((p7.ok || dense_plan(g)) ? 0 : sizeof(float) * (size_t)g.M * g.K));
   W.total = o;
   return W;
 }
@@ -629,16 +618,13 @@ int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa,
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
 // shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words
-// (interleaved 3-bit words: w2a2 / w3a3; other slice counts take the general backward)
-inline bool shift_stats_ok(const Geo& g) {
-  return shift_fast(g) && g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
-}
+// (shift_stats_ok, above ws_layout; other layers take the general backward)
 int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
                        const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s,
                        int accum_beta = 0);
 int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
                      hipStream_t s);
-// cimq_part_bwd.hip: backward of layers outside the v7 plan (v5 / v6 and general kernels)
+// cimq_part_bwd.hip: backward of layers outside the v7 / dense plans (the general kernels)
 int launch_bwd_general(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                        const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused);
 // cimq_part_bwd.hip: per-chunk sums of |ps * sw * sa| for the alpha_cim initialisation

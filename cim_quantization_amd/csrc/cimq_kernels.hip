@@ -367,27 +367,6 @@ __device__ inline void wcy_item(const Geo& g, const WSrc& ws, int ncpbt, v4i* __
   wcy[t] = o;
 }
 
-// grad_x transposed-GEMM operand: int8(slice) as bf16 in [i][khw][c (Cp)][kappa (NKS*32)] order,
-// one copy per tile i with the rows of other tiles zeroed, so a kernel stages a tile's rows
-// by plain copy.  Row (i, khw, c) = weight row f = c*KHW + khw; one 16-B piece holds 8
-// consecutive kappa.
-__device__ inline void wtc_item(const Geo& g, const WSrc& ws, int Cp, uint4* __restrict__ wtc, int t) {
-  const int KAP = g.NKS * 32;
-  const int piece = t % (KAP / 8), row = t / (KAP / 8);
-  const int i = row / (g.KHW * Cp), rr = row - i * (g.KHW * Cp);
-  const int khw = rr / Cp, c = rr - khw * Cp;
-  const int f = c * g.KHW + khw;
-  const bool in_tile = c < g.C && f >= i * g.xbar && f < min(g.K, (i + 1) * g.xbar);
-  uint32_t wd[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int kap = piece * 8 + e;
-    float val = 0.f;
-    if (in_tile && kap < g.NBLK * 16) val = (float)to_i8_wrap(wslice(g, ws, f, kap));
-    wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
-  }
-  wtc[t] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-}
 
 #ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
 __global__ void prep_wfrag_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p,
@@ -416,16 +395,6 @@ __global__ void prep_wcy_kernel(Geo g, const float* __restrict__ w_q, const floa
   const int total = g.T * ncpbt * g.NKS * WAVE;
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
     wcy_item(g, ws, ncpbt, wcy, t);
-}
-#endif
-
-#ifdef CIMQ_TU_MAIN  // non-template kernel: defined in one translation unit only
-__global__ void prep_wtc_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int Cp,
-                                uint4* __restrict__ wtc) {
-  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
-  const int total = g.T * g.KHW * Cp * (g.NKS * 32 / 8);
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
-    wtc_item(g, ws, Cp, wtc, t);
 }
 #endif
 
@@ -578,7 +547,7 @@ __global__ void prep_params_kernel(Geo g, const float* __restrict__ alpha_q, con
   const ASrc as{alpha_q, 0, 0.f, 0.f};
   const int total = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba + (beta != nullptr ? g.Opad : 0);
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x)
-    if (params_item(g, as, sw, sa, bmask, pp, t, beta)) atomicOr(&pp.flags[0], 1);
+    if (params_item(g, as, sw, sa, bmask, pp, t, beta)) pp.flags[0] = 1;  // every writer stores 1
 }
 #endif
 
@@ -809,186 +778,176 @@ __global__ __launch_bounds__(256) void cim_fwd_kernel(Geo g, const int8_t* __res
 // =========================================================================================
 // cim_bwd_gx: grad wrt the activation   (lsq.py:338-382, closed form)
 // =========================================================================================
-//   gx_unf[m,f] = (sw/nba) * sum_{k,o} g[m,o] * E_k[m,i(f),o] * w^_k[f,o]
+//   gx_unf[m,f] = sum_{k,o} g[m,o] * E_k[m,i(f),o] * w^_k[f,o]
 //   E_k = sum_j 2^-(bsa*j) * mask[k,j] * STE[m,i,k,j,o]
 // ps is recomputed TRANSPOSED (rows kappa=(k,o), columns = pixels) so each accumulator is
 // directly the B operand of the next bf16 MFMA (contraction over kappa, no LDS transpose);
-// g*E is split into three bf16 terms.  The im2col adjoint (nn.Fold) is an LDS scatter-add
-// into the block's image (LDS_ACC) or, for images too large for LDS, global atomics.
-template <int NBP, int FBMAX, bool LDS_ACC>
+// g*E is split into three bf16 terms.  Block = (64 pixels, crossbar tile blockIdx.y): the
+// tiles' f ranges are disjoint, so every unfolded value gxu[m][f] is written by exactly one
+// lane; fold_gx_kernel then applies the nn.Fold adjoint (lsq.py:382) in a fixed order -- no
+// atomics anywhere, bit-identical run to run.
+template <int NBP, int FBMAX>
 __global__ __launch_bounds__(256) void cim_bwd_gx_kernel(Geo g, const int8_t* __restrict__ xcode,
                                                          const v4i* __restrict__ wfrag,
                                                          const v4i* __restrict__ wgx, Params pp,
                                                          const float* __restrict__ sw_p,
                                                          const float* __restrict__ sa_p,
                                                          const float* __restrict__ gout,
-                                                         float* __restrict__ gx) {
+                                                         float* __restrict__ gxu) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   TileSmem sm;
   sm.As = reinterpret_cast<int8_t*>(smem);
   size_t off = (size_t)g.nba * 64 * g.KTP;
   sm.foff = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
   sm.fkk = reinterpret_cast<int*>(smem + off); off += sizeof(int) * g.KS * 64;
-  sm.rowinfo = reinterpret_cast<int4*>(smem + off); off += sizeof(int4) * 64;
-  float* gxacc = reinterpret_cast<float*>(smem + off);  // [C*H*W] when LDS_ACC
+  sm.rowinfo = reinterpret_cast<int4*>(smem + off);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sw = *sw_p, sa = *sa_p;
   const bool literal = (pp.flags[0] != 0) || g.variant != VAR_LIBRARY;
   const int nkj = g.nbw * g.nba;
-  const int chw = g.C * g.HW;
+  const int m0 = blockIdx.x * 64;
+  const int i = blockIdx.y;
+  const int flo = i * g.xbar, flen = min(g.xbar, g.K - flo);
 
-  int mbeg, mend;
-  if (LDS_ACC) {
-    const int b = blockIdx.x;
-    mbeg = b * g.P;
-    mend = mbeg + g.P;
-    for (int t = threadIdx.x; t < chw; t += blockDim.x) gxacc[t] = 0.f;
-  } else {
-    mbeg = blockIdx.x * 64;
-    mend = min(mbeg + 64, g.M);
-  }
+  build_rowinfo(g, m0, sm.rowinfo);
+  build_ftable(g, i, sm.foff, sm.fkk);
+  __syncthreads();
+  build_As<NBP>(g, xcode, sm);
+  __syncthreads();
 
-  // global-accumulator blocks own one crossbar tile each (blockIdx.y): the tiles' f ranges are
-  // disjoint, so the grid has T times more blocks for the same work
-  const int i_lo = LDS_ACC ? 0 : (int)blockIdx.y, i_hi = LDS_ACC ? g.T : (int)blockIdx.y + 1;
-  for (int m0 = mbeg; m0 < mend; m0 += 64) {
-    __syncthreads();
-    build_rowinfo(g, m0, sm.rowinfo);
-    if (LDS_ACC && threadIdx.x < 64 && m0 + (int)threadIdx.x >= mend) sm.rowinfo[threadIdx.x].w = 0;
-    for (int i = i_lo; i < i_hi; ++i) {
-      __syncthreads();
-      build_ftable(g, i, sm.foff, sm.fkk);
-      __syncthreads();
-      build_As<NBP>(g, xcode, sm);
-      __syncthreads();
-
-      const int mcol = m0 + wave * 16 + r16;  // this lane's pixel (accumulator column)
-      const bool mvalid = sm.rowinfo[wave * 16 + r16].w != 0;
-      v4f gxa[FBMAX];
+  const int mcol = m0 + wave * 16 + r16;  // this lane's pixel (accumulator column)
+  const bool mvalid = sm.rowinfo[wave * 16 + r16].w != 0;
+  v4f gxa[FBMAX];
 #pragma unroll
-      for (int fb = 0; fb < FBMAX; ++fb) gxa[fb] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int fb = 0; fb < FBMAX; ++fb) gxa[fb] = v4f{0.f, 0.f, 0.f, 0.f};
 
-      for (int kc = 0; kc < g.NBLK; kc += 8) {  // chunk of 8 kappa-blocks (4 MFMA K-steps)
-        float E[8][4];
+  for (int kc = 0; kc < g.NBLK; kc += 8) {  // chunk of 8 kappa-blocks (4 MFMA K-steps)
+    float E[8][4];
 #pragma unroll
-        for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < 8; ++a)
 #pragma unroll
-          for (int b = 0; b < 4; ++b) E[a][b] = 0.f;
-        for (int j = 0; j < g.nba; ++j) {
-          v4i xb[4];
+      for (int b = 0; b < 4; ++b) E[a][b] = 0.f;
+    for (int j = 0; j < g.nba; ++j) {
+      v4i xb[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        if (ks < g.KS) xb[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int kb = kc + kk;
+        if (kb < g.NBLK) {
+          v4i acc = {0, 0, 0, 0};
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks)
-            if (ks < g.KS) xb[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
+            if (ks < g.KS)
+              acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                  wfrag[((size_t)(i * g.KS + ks) * g.NBLK + kb) * WAVE + lane], xb[ks], acc, 0, 0, 0);
+          const int k = kb / g.OB16;
+          const int obase = (kb - k * g.OB16) * 16 + 4 * g4;
+          const float ce = pp.ckj[nkj + k * g.nba + j];
+          const int pi = pidx(g, i, j, k, obase);
 #pragma unroll
-          for (int kk = 0; kk < 8; ++kk) {
-            const int kb = kc + kk;
-            if (kb < g.NBLK) {
-              v4i acc = {0, 0, 0, 0};
-#pragma unroll
-              for (int ks = 0; ks < 4; ++ks)
-                if (ks < g.KS)
-                  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                      wfrag[((size_t)(i * g.KS + ks) * g.NBLK + kb) * WAVE + lane], xb[ks], acc, 0, 0, 0);
-              const int k = kb / g.OB16;
-              const int obase = (kb - k * g.OB16) * 16 + 4 * g4;
-              const float ce = pp.ckj[nkj + k * g.nba + j];
-              const int pi = pidx(g, i, j, k, obase);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                bool pass;
-                if (!literal) {
-                  pass = (unsigned)(acc[r] - pp.mlo[pi + r]) <= (unsigned)pp.mhi[pi + r];
-                } else {
-                  const float b = psb_value(g, acc[r], sw, sa, pp.alpha[pi + r], pp.beta[pi + r]);
-                  pass = ste_pass(b, g.thr_hi, g.thr_lo);
-                }
-                E[kk][r] += pass ? ce : 0.f;
-              }
+          for (int r = 0; r < 4; ++r) {
+            bool pass;
+            if (!literal) {
+              pass = (unsigned)(acc[r] - pp.mlo[pi + r]) <= (unsigned)pp.mhi[pi + r];
+            } else {
+              const float b = psb_value(g, acc[r], sw, sa, pp.alpha[pi + r], pp.beta[pi + r]);
+              pass = ste_pass(b, g.thr_hi, g.thr_lo);
             }
-          }
-        }
-        // B operands: (g * E)[kappa, pixel], kappa-step s covers kappa-blocks kc+2s, kc+2s+1
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int kb0 = kc + 2 * s;
-          if (kb0 < g.NBLK) {
-            uint32_t hi[4] = {0, 0, 0, 0}, mi[4] = {0, 0, 0, 0}, lo[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int kb = kb0 + (e >> 2);
-              const int r = e & 3;
-              float av = 0.f;
-              if (kb < g.NBLK && mvalid) {
-                const int k = kb / g.OB16;
-                const int o = (kb - k * g.OB16) * 16 + 4 * g4 + r;
-                if (o < g.O) av = gout[(size_t)mcol * g.O + o] * E[2 * s + (e >> 2)][r];
-              }
-              uint16_t h, md, l;
-              split3(av, h, md, l);
-              hi[e >> 1] |= (uint32_t)h << (16 * (e & 1));
-              mi[e >> 1] |= (uint32_t)md << (16 * (e & 1));
-              lo[e >> 1] |= (uint32_t)l << (16 * (e & 1));
-            }
-            const v8bf bh = as_v8bf(v4i{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]});
-            const v8bf bm = as_v8bf(v4i{(int)mi[0], (int)mi[1], (int)mi[2], (int)mi[3]});
-            const v8bf bl = as_v8bf(v4i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]});
-            const int sg = kc / 2 + s;
-#pragma unroll
-            for (int fb = 0; fb < FBMAX; ++fb) {
-              if (fb < g.FBT) {
-                const v8bf wa = as_v8bf(wgx[((size_t)(i * g.FBT + fb) * g.NKS + sg) * WAVE + lane]);
-                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bh, gxa[fb], 0, 0, 0);
-                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bm, gxa[fb], 0, 0, 0);
-                gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bl, gxa[fb], 0, 0, 0);
-              }
-            }
+            E[kk][r] += pass ? ce : 0.f;
           }
         }
       }
-      // scatter gx_unf[f, pixel] -> image (col2im / nn.Fold adjoint of the unfold)
-      if (mvalid) {
-        const int4 ri = sm.rowinfo[wave * 16 + r16];
+    }
+    // B operands: (g * E)[kappa, pixel], kappa-step s covers kappa-blocks kc+2s, kc+2s+1
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kb0 = kc + 2 * s;
+      if (kb0 < g.NBLK) {
+        uint32_t hi[4] = {0, 0, 0, 0}, mi[4] = {0, 0, 0, 0}, lo[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int kb = kb0 + (e >> 2);
+          const int r = e & 3;
+          float av = 0.f;
+          if (kb < g.NBLK && mvalid) {
+            const int k = kb / g.OB16;
+            const int o = (kb - k * g.OB16) * 16 + 4 * g4 + r;
+            if (o < g.O) av = gout[(size_t)mcol * g.O + o] * E[2 * s + (e >> 2)][r];
+          }
+          uint16_t h, md, l;
+          split3(av, h, md, l);
+          hi[e >> 1] |= (uint32_t)h << (16 * (e & 1));
+          mi[e >> 1] |= (uint32_t)md << (16 * (e & 1));
+          lo[e >> 1] |= (uint32_t)l << (16 * (e & 1));
+        }
+        const v8bf bh = as_v8bf(v4i{(int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]});
+        const v8bf bm = as_v8bf(v4i{(int)mi[0], (int)mi[1], (int)mi[2], (int)mi[3]});
+        const v8bf bl = as_v8bf(v4i{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3]});
+        const int sg = kc / 2 + s;
 #pragma unroll
         for (int fb = 0; fb < FBMAX; ++fb) {
           if (fb < g.FBT) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int t = fb * 16 + 4 * g4 + r;
-              const int fk = (t < g.KS * 64) ? sm.fkk[t] : -1;
-              if (fk >= 0) {
-                const int ih = ri.y + (fk >> 16), iw = ri.z + (fk & 0xFFFF);
-                if (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) {
-                  const float v = gxa[fb][r];
-                  if (LDS_ACC) {
-                    const int b = mcol / g.P;
-                    atomicAdd(&gxacc[ri.x - b * chw + sm.foff[t]], v);
-                  } else {
-                    atomicAdd(&gx[(size_t)ri.x + sm.foff[t]], v);
-                  }
-                }
-              }
-            }
+            const v8bf wa = as_v8bf(wgx[((size_t)(i * g.FBT + fb) * g.NKS + sg) * WAVE + lane]);
+            gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bh, gxa[fb], 0, 0, 0);
+            gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bm, gxa[fb], 0, 0, 0);
+            gxa[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bl, gxa[fb], 0, 0, 0);
           }
         }
       }
     }
   }
-  if (LDS_ACC) {
-    __syncthreads();
-    const float scale = sw / (float)g.nba;
-    const size_t base = (size_t)blockIdx.x * chw;
-    for (int t = threadIdx.x; t < chw; t += blockDim.x) gx[base + t] = gxacc[t] * scale;
+  // gx_unf[pixel, f] of this tile's rows (accumulator row fb*16 + 4*g4 + r, column = pixel)
+  if (mvalid) {
+    float* dst = gxu + (size_t)mcol * g.K + flo;
+#pragma unroll
+    for (int fb = 0; fb < FBMAX; ++fb) {
+      if (fb < g.FBT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = fb * 16 + 4 * g4 + r;
+          if (t < flen) dst[t] = gxa[fb][r];
+        }
+      }
+    }
   }
 }
 
+// nn.Fold adjoint of the unfold (lsq.py:382): every input element sums its (kh, kw) window
+// taps of gx_unf in a fixed order, times sw / nba (lsq.py:362-376's slice recombination).
+// Dilation is ignored, as by the reference's Unfold of the forward (lsq.py:141).
 #ifdef CIMQ_TU_BWD  // non-template kernel: defined in one translation unit only
-__global__ void scale_kernel(float* __restrict__ v, long long n, const float* __restrict__ sw_p, int nba) {
-  const float scale = (*sw_p) / (float)nba;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    v[i] *= scale;
+__global__ void fold_gx_kernel(Geo g, const float* __restrict__ gxu, const float* __restrict__ sw_p,
+                               float* __restrict__ gx) {
+  const float scale = (*sw_p) / (float)g.nba;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < g.Nin;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int iw = (int)(idx % g.W);
+    long long r = idx / g.W;
+    const int ih = (int)(r % g.H);
+    r /= g.H;
+    const int c = (int)(r % g.C);
+    const int b = (int)(r / g.C);
+    float a = 0.f;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int th = ih + g.PH - kh;
+      if (th < 0 || th % g.SH != 0) continue;
+      const int oh = th / g.SH;
+      if (oh >= g.Ho) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int tw = iw + g.PW - kw;
+        if (tw < 0 || tw % g.SW != 0) continue;
+        const int ow = tw / g.SW;
+        if (ow >= g.Wo) continue;
+        const size_t m = (size_t)b * g.P + (size_t)oh * g.Wo + ow;
+        a += gxu[m * g.K + (size_t)c * g.KHW + kh * g.KW + kw];
+      }
+    }
+    gx[idx] = a * scale;
+  }
 }
 #endif
 
@@ -1023,15 +982,14 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const int tlen = g.KS * 64;
   const int nkj = g.nbw * g.nba;
   const int ncol = 32;
-  // [nkj][32]: sum code*g; INIT: [4 waves][nkj][32] sums of |u|, one writer per slot and
-  // added in wave order at the end (bit-reproducible alpha_cim init); the extra rows
-  // overlap gwacc / Xb, which INIT does not use (lds_gw leaves room: nba*KS*4096 >= 384*nkj)
+  // [4 waves][nkj][32]: sums of code*g (INIT: of |u|), one writer lane per slot and wave, the
+  // waves added in a fixed order at the end -- no atomics, bit-identical run to run
   float* qacc = reinterpret_cast<float*>(smem + off);
-  off += sizeof(float) * nkj * ncol;
+  off += sizeof(float) * 4 * nkj * ncol;
   float* gwacc = reinterpret_cast<float*>(smem + off);  // [FBT*16][32]
   off += sizeof(float) * g.FBT * 16 * ncol;
-  float* qbacc = reinterpret_cast<float*>(smem + off);  // [nkj][32]: sum beta_term*g (shift variants)
-  off += sizeof(float) * nkj * ncol;
+  float* qbacc = reinterpret_cast<float*>(smem + off);  // [4 waves][nkj][32]: sum beta_term*g (shift variants)
+  off += sizeof(float) * 4 * nkj * ncol;
   int8_t* Xb = reinterpret_cast<int8_t*>(smem + off);   // [nba][tlen][64] bwd slices, f-major
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1047,9 +1005,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const bool has_code = has_alpha(g);
   const bool shift = is_shift(g);
 
-  for (int t = threadIdx.x; t < nkj * ncol * (INIT ? 4 : 1); t += blockDim.x) qacc[t] = 0.f;
+  for (int t = threadIdx.x; t < 4 * nkj * ncol; t += blockDim.x) qacc[t] = 0.f;
   if (!INIT)
-    for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) qbacc[t] = 0.f;
+    for (int t = threadIdx.x; t < 4 * nkj * ncol; t += blockDim.x) qbacc[t] = 0.f;
   if (!INIT)
     for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
   v4f gwa[FBMAX][2];
@@ -1160,11 +1118,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                 qb += __shfl_xor(qb, 16);
                 qb += __shfl_xor(qb, 32);
               }
-              if (INIT) {
-                if (g4 == 0) qacc[(wave * nkj + kj) * ncol + ocol] += qs;
-              } else if (g4 == 0 && has_code) {
-                atomicAdd(&qacc[kj * ncol + ocol], qs);
-                if (shift) atomicAdd(&qbacc[kj * ncol + ocol], qb);
+              if (g4 == 0 && (INIT || has_code)) {
+                qacc[(wave * nkj + kj) * ncol + ocol] += qs;
+                if (!INIT && shift) qbacc[(wave * nkj + kj) * ncol + ocol] += qb;
               }
             }
           }
@@ -1221,28 +1177,34 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
     }
   }
 
-  // ---- block reductions -> slabs (deterministic across blocks; in-block LDS order) ----
+  // ---- block reductions -> slabs (deterministic: the waves in a fixed order, no atomics) ----
   if (!INIT) {
+    for (int w = 0; w < 4; ++w) {
+      __syncthreads();
+      if (wave == w) {
 #pragma unroll
-    for (int fb = 0; fb < FBMAX; ++fb)
-      if (fb < g.FBT)
+        for (int fb = 0; fb < FBMAX; ++fb)
+          if (fb < g.FBT)
 #pragma unroll
-        for (int ob = 0; ob < 2; ++ob)
-          if (ob < nob)
+            for (int ob = 0; ob < 2; ++ob)
+              if (ob < nob)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * ncol + ob * 16 + r16], gwa[fb][ob][r]);
+                for (int r = 0; r < 4; ++r) gwacc[(fb * 16 + 4 * g4 + r) * ncol + ob * 16 + r16] += gwa[fb][ob][r];
+      }
+    }
   }
   __syncthreads();
+  const int wq = nkj * ncol;
   for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) {
     const int q = t / ncol, col = t - q * ncol;
     const int o = og * 32 + col;
     if (o < g.Opad) {
       const int k = q / g.nba, j = q - k * g.nba;
-      float qv = qacc[t];
-      if (INIT) qv = ((qv + qacc[nkj * ncol + t]) + qacc[2 * nkj * ncol + t]) + qacc[3 * nkj * ncol + t];
+      const float qv = ((qacc[t] + qacc[wq + t]) + qacc[2 * wq + t]) + qacc[3 * wq + t];
       ga_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qv;
-      if (!INIT && shift) gb_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] = qbacc[t];
+      if (!INIT && shift)
+        gb_slab[(((size_t)mc * g.T + i) * nkj + (size_t)k * g.nba + j) * g.Opad + o] =
+            ((qbacc[t] + qbacc[wq + t]) + qbacc[2 * wq + t]) + qbacc[3 * wq + t];
     }
   }
   if (INIT) return;

@@ -48,17 +48,6 @@ __device__ inline int fdiv(int n, int d, float inv) {
 
 __device__ inline size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 
-// grad_out of the 4 pixels m4 .. m4+3 (a quad inside one image, m4 % 4 == 0) for channel o,
-// in either layout (Geo::onchw); NCHW makes it one 16-B load
-__device__ inline float4 load_g4(const Geo& g, const float* __restrict__ gout, size_t m4, int o) {
-  if (g.onchw) {
-    const size_t b = m4 / g.P, p = m4 - b * g.P;
-    return *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p);
-  }
-  return make_float4(gout[m4 * g.O + o], gout[(m4 + 1) * g.O + o], gout[(m4 + 2) * g.O + o],
-                     gout[(m4 + 3) * g.O + o]);
-}
-
 // Batched global -> LDS copy: every thread issues U independent loads before its first LDS
 // store, so a block waits about one memory latency per U*blockDim elements instead of one
 // per element.  src(idx) returns element idx; it lands in dst[idx].
@@ -124,53 +113,6 @@ __device__ inline void stage_rows(const Geo& g, int WP, int RHx, const uint8_t* 
       if (d[u] >= 0) {
         uint32_t* p = reinterpret_cast<uint32_t*>(patch + d[u]);
         p[0] = v[u].x; p[1] = v[u].y; p[2] = v[u].z; p[3] = v[u].w;
-      }
-    }
-  }
-}
-
-// the same rows of the backward ctx slices, widened to bf16 (exact small integers):
-// element word = NBP bf16 = NBP/2 dwords, dword s = {bf16(slice 2s), bf16(slice 2s+1)}
-__device__ inline uint32_t bf16x2_of_bytes(uint32_t w, int sh) {
-  const float lo = (float)(int8_t)((w >> sh) & 0xFF);
-  const float hi = (float)(int8_t)((w >> (sh + 8)) & 0xFF);
-  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
-}
-
-template <int NBP>
-__device__ inline void stage_rows_bf16(const Geo& g, int WP, int RHx, const uint8_t* __restrict__ xc, int b,
-                                       int ih_first, uint8_t* patch, int c0 = 0, int ncx = -1) {
-  const int QW = g.W * NBP / 16;
-  const int n = (ncx < 0 ? g.C : ncx) * RHx * QW;
-  const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
-  const uint4* src = reinterpret_cast<const uint4*>(xc) + ((size_t)b * g.C + c0) * g.H * QW;
-  const int nt = blockDim.x;
-  for (int base = threadIdx.x; base < n; base += 4 * nt) {
-    uint4 v[4];
-    int d[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = base + u * nt;
-      d[u] = -1;
-      if (idx < n) {
-        const int row = fdiv(idx, QW, invQ), q = idx - row * QW;
-        const int c = fdiv(row, RHx, invR), rr = row - c * RHx;
-        const int ih = ih_first + rr;
-        d[u] = ((c * RHx + rr) * WP + g.PW) * (2 * NBP) + q * 32;
-        v[u] = make_uint4(0, 0, 0, 0);
-        if (ih >= 0 && ih < g.H) v[u] = src[((size_t)c * g.H + ih) * QW + q];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (d[u] >= 0) {
-        uint32_t* p = reinterpret_cast<uint32_t*>(patch + d[u]);
-        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          p[2 * e] = bf16x2_of_bytes(w[e], 0);
-          p[2 * e + 1] = bf16x2_of_bytes(w[e], 16);
-        }
       }
     }
   }
@@ -291,16 +233,8 @@ __device__ __noinline__ uint32_t shift_state_literal(int p, float sw, float sa, 
 // forward: out[m, o] = sum_{i,j,k} ADC(ps_ijk[m, o]) * mask   (lsq.py:166-233)
 // block = 64-pixel m-tiles (grid-stride) x one 64-wide o-group; wave w = pixels 16w..16w+15.
 // ---------------------------------------------------------------------------------------
-// State words (what the backward needs of every partial sum, instead of the partial sum):
-// st[i][k][m/4][o][m%4], SB = 2 bytes for nba <= 5 else 4; for bit slice j, bit 3j = STE
-// pass (lsq.py:310-313), bit 3j+1 = ADC code != 0, bit 3j+2 = ADC code < 0 (lsq.py:321-332).
-template <int NBP>
-struct StWord;
-template <>
-struct StWord<4> { typedef uint16_t T; };
-template <>
-struct StWord<8> { typedef uint32_t T; };
-
+// state bits of one partial sum: bit 0 STE pass (lsq.py:310-313), bit 1 ADC code != 0, bit 2
+// ADC code < 0 (lsq.py:321-332)
 __device__ inline uint32_t st_bits(bool pass, float code) {
   return (pass ? 1u : 0u) | ((code != 0.f) ? 2u : 0u) | ((code < 0.f) ? 4u : 0u);
 }
@@ -332,7 +266,6 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                                                          const float* __restrict__ sw_p,
                                                          const float* __restrict__ sa_p, float* __restrict__ out,
                                                          uint8_t* __restrict__ st) {
-  typedef typename StWord<NBP>::T SW;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int og = blockIdx.y;
   const int NOB = min(OBM, g.OB16);
@@ -354,7 +287,6 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   const bool literal = flag_lit || g.mode != ADC_TERNARY;
   const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
   const int Wo = 1 << v.lw;
-  const size_t MQ = (size_t)g.M >> 2;
 
   // index math by shifts (NOB in {1, 2, 4}, KS in {1, 2}) and a float-reciprocal division
   // by nbw: integer division is ~30 VALU each, and this prologue runs once per block
@@ -612,15 +544,6 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #pragma unroll
               for (int r = 0; r < 4; ++r) stc[ob][r] |= stw[r] << (3 * g.nba * k);
             }
-            // state words of pixels wave*16 + 4*g4 + (0..3), channel o: one 4-pixel quad
-            if (!CST && o < g.O) {
-              const size_t q = ((size_t)(i * g.nbw + k) * MQ + (size_t)mt * 16 + wave * 4 + g4) * g.O + o;
-              if (sizeof(SW) == 2) {
-                reinterpret_cast<uint2*>(st)[q] = make_uint2(stw[0] | (stw[1] << 16), stw[2] | (stw[3] << 16));
-              } else {
-                reinterpret_cast<uint4*>(st)[q] = make_uint4(stw[0], stw[1], stw[2], stw[3]);
-              }
-            }
           }
         }
       }
@@ -668,846 +591,6 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
         }
       }
     }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// grad_x (+ fused LSQ activation backward) as a transposed implicit GEMM: block = one band of
-// RI input rows of one image.  Per tile i and 32-wide kappa chunk:
-//   phase A  G_i[m, kappa] = g[m, o] * E_i[m, kappa],  E_i = sum_j cE_kj * STE_ijk[m, o]
-//            for every output pixel m touching the band, from the forward's state words,
-//            split into bf16 hi/mid/lo rows in LDS;
-//   phase B  gx[q, c] += sum_{kh,kw} sum_kappa G_i[m(q,kh,kw), kappa] * int8(w_k[(c,kh,kw), o])
-//            on bf16 MFMA, q = input position of the band, c = channel (lsq.py:257-317).
-// The nn.Fold adjoint is folded into the MFMA K dimension (kh, kw, kappa): every wave owns
-// its output tiles in registers for the whole kernel, so there are no atomics; the LSQ
-// activation backward is applied in registers and gx stored once.
-// ---------------------------------------------------------------------------------------
-template <int NBP, int TPW, bool LSQ>
-__global__ __launch_bounds__(512, 2) void cim_bwd_gx_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
-                                                            const uint4* __restrict__ wtc, Params pp,
-                                                            const float* __restrict__ sw_p,
-                                                            const float* __restrict__ sa_p,
-                                                            const float* __restrict__ gout,
-                                                            const float* __restrict__ x, float* __restrict__ gx,
-                                                            float* __restrict__ gsa_part) {
-  typedef typename StWord<NBP>::T SW;
-  // TPW: output tiles per wave (host guarantees NT <= 8 * TPW)
-  constexpr int GP = 32;    // G row pitch in bf16 (consecutive A-operand rows are contiguous)
-  constexpr int WPB = 40;   // W row pitch in bf16: 32 kappa + 8 pad (bank spread)
-  constexpr int KX = 3;     // max kernel height / width (host guarantees KH, KW <= 3)
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int nkj = g.nbw * g.nba;
-  const int b = blockIdx.x / v.nbands, band = blockIdx.x - b * v.nbands;
-  const int r0 = band * v.RI, r1 = min(g.H, r0 + v.RI);
-  const int nrow = r1 - r0;
-  int oh_lo = r0 + g.PH - (g.KH - 1);
-  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.SH - 1) / g.SH;
-  const int oh_hi = min(g.Ho - 1, (r1 - 1 + g.PH) / g.SH);
-  const int nro = oh_hi - oh_lo + 1;
-  const int npb = nro << v.lw;
-  const int Cp = v.CB * 16;
-  const int ZROW = v.NPB;  // all-zero G row
-  const int PART = (v.NPB + 1) * GP;  // bf16 elements per split part
-
-  uint8_t* cur = smem;
-  __bf16* Gs = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)3 * PART * 2);          // [part][row][GP]
-  __bf16* Wb = reinterpret_cast<__bf16*>(cur); cur += al16((size_t)g.KHW * Cp * WPB * 2);   // [khw][c][WPB]
-  float* ckl = reinterpret_cast<float*>(cur); cur += al16(3 * nkj * 4);
-  float* red = reinterpret_cast<float*>(cur);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, NW = blockDim.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const float sw = *sw_p, sa = *sa_p;
-  const bool gvec = (g.O & 3) == 0;
-  const size_t MQ = (size_t)g.M >> 2;
-  const size_t m_band = (size_t)b * g.P + ((size_t)oh_lo << v.lw);  // first output pixel of the band
-
-  for (int t = threadIdx.x; t < 3 * GP / 2; t += blockDim.x) {
-    const int part = t / (GP / 2), w = t - part * (GP / 2);
-    reinterpret_cast<uint32_t*>(Gs + part * PART + ZROW * GP)[w] = 0u;
-  }
-  for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
-
-  // this wave's output tiles: t = wave + NW*u -> (q-block, c-block); the lane's A-operand
-  // position q = qb*16 + r16 and its four accumulator positions q = qb*16 + 4*g4 + r
-  const int nq = nrow * g.W;
-  const int QBb = (nq + 15) >> 4;
-  const int NTb = QBb * v.CB;
-  int ihp[TPW], iwp[TPW];
-  float xpre[TPW][4];
-  v4f acc[TPW];
-#pragma unroll
-  for (int u = 0; u < TPW; ++u) {
-    acc[u] = v4f{0.f, 0.f, 0.f, 0.f};
-    const int t = wave + NW * u;
-    const int qb = t / v.CB, cb = t - qb * v.CB;
-    const int q = qb * 16 + r16;
-    const int ih = r0 + q / g.W, iw = q - (q / g.W) * g.W;
-    ihp[u] = (t < NTb && q < nq) ? ih + g.PH - oh_lo * g.SH : -(1 << 20);
-    iwp[u] = iw + g.PW;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qa = qb * 16 + 4 * g4 + r, c = cb * 16 + r16;
-      xpre[u][r] = 0.f;
-      if (LSQ && t < NTb && qa < nq && c < g.C) xpre[u][r] = x[(((size_t)b * g.C + c) * g.H + r0) * g.W + qa];
-    }
-  }
-  // G row of every (tile, tap) for this lane's A-operand position (the zero row when the
-  // output pixel does not exist); in registers for two tiles per wave
-  constexpr int RIX = (TPW <= 2) ? TPW * KX * KX : 1;
-  int rowidx[RIX];
-  auto grow_of = [&](int u, int kh, int kw) -> int {
-    const int ohs = ihp[u] - kh, ows = iwp[u] - kw;
-    int row = ZROW;
-    if (ohs >= 0 && ows >= 0 && (ohs % g.SH) == 0 && (ows % g.SW) == 0) {
-      const int oh = ohs / g.SH, ow = ows / g.SW;
-      if (oh < nro && ow < g.Wo) row = (oh << v.lw) + ow;
-    }
-    return row;
-  };
-  if constexpr (TPW <= 2) {
-#pragma unroll
-    for (int u = 0; u < TPW; ++u)
-#pragma unroll
-      for (int kh = 0; kh < KX; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < KX; ++kw) rowidx[(u * KX + kh) * KX + kw] = grow_of(u, kh, kw);
-  }
-
-  const int nquad = npb >> 2;          // 4-pixel quads of the band
-  const float invOB = 1.f / (float)g.OB16;
-
-  for (int i = 0; i < g.T; ++i) {
-    const int ci0 = (i * g.xbar) / g.KHW, ci1 = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
-    for (int kc = 0; kc < g.NKS; ++kc) {
-      __syncthreads();
-      // W rows of this tile and kappa chunk: Wb[khw][c][kappa] (zero for (c, khw) outside tile i)
-      {
-        const int nvec = g.KHW * Cp * 4;  // 16-B pieces: 4 data pieces per (khw, c) row
-        for (int base = threadIdx.x; base < nvec; base += 4 * blockDim.x) {
-          uint4 val[4];
-          int dst[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int idx = base + u * blockDim.x;
-            dst[u] = -1;
-            if (idx < nvec) {
-              const int row = idx >> 2, q8 = idx & 3;  // row = khw * Cp + c
-              const int khw = row / Cp, c = row - khw * Cp;
-              const int f = c * g.KHW + khw;
-              val[u] = make_uint4(0, 0, 0, 0);
-              if (c < g.C && f >= i * g.xbar && f < min(g.K, (i + 1) * g.xbar))
-                val[u] = wtc[(((size_t)i * g.KHW * Cp + row) * g.NKS + kc) * 4 + q8];
-              dst[u] = row * (WPB / 8) + q8;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (dst[u] >= 0) reinterpret_cast<uint4*>(Wb)[dst[u]] = val[u];
-        }
-      }
-      // phase A: one item = 4 pixels x 4 consecutive kappa (same k, 4 channels)
-      for (int it = threadIdx.x; it < nquad * 8; it += blockDim.x) {
-        const int qd = it >> 3, kq = it & 7;
-        const int kb = 2 * kc + (kq >> 2);
-        float G[4][4];  // [pixel r][channel e]
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) G[r][e] = 0.f;
-        if (kb < g.NBLK) {
-          const int k = fdiv(kb, g.OB16, invOB);
-          const int o0 = (kb - k * g.OB16) * 16 + (kq & 3) * 4;
-          const size_t m0 = m_band + 4 * (size_t)qd;
-          // state words of 4 pixels for channels o0..o0+3 (16 words, contiguous)
-          SW sv[4][4];
-          if (gvec && o0 + 4 <= g.O) {
-            const size_t q = ((size_t)(i * g.nbw + k) * MQ + (m0 >> 2)) * g.O + o0;
-            if (sizeof(SW) == 2) {
-              const uint4 a0 = reinterpret_cast<const uint4*>(st + q * 8)[0];
-              const uint4 a1 = reinterpret_cast<const uint4*>(st + q * 8)[1];
-              const uint32_t w8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) sv[e][r] = (SW)(w8[2 * e + (r >> 1)] >> (16 * (r & 1)));
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const uint4 a = reinterpret_cast<const uint4*>(st)[q + e];
-                sv[e][0] = a.x; sv[e][1] = a.y; sv[e][2] = a.z; sv[e][3] = a.w;
-              }
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                sv[e][r] = 0;
-                if (o0 + e < g.O)
-                  sv[e][r] = reinterpret_cast<const SW*>(st)[(((size_t)(i * g.nbw + k) * MQ + (m0 >> 2)) * g.O + o0 + e) * 4 + r];
-              }
-          }
-          float gv[4][4];
-          if (g.onchw) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
-              if (o0 + e < g.O) t4 = load_g4(g, gout, m0, o0 + e);
-              gv[0][e] = t4.x; gv[1][e] = t4.y; gv[2][e] = t4.z; gv[3][e] = t4.w;
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float* grow = gout + (m0 + r) * g.O;
-              if (gvec && o0 + 4 <= g.O) {
-                const float4 t4 = *reinterpret_cast<const float4*>(grow + o0);
-                gv[r][0] = t4.x; gv[r][1] = t4.y; gv[r][2] = t4.z; gv[r][3] = t4.w;
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) gv[r][e] = (o0 + e < g.O) ? grow[o0 + e] : 0.f;
-              }
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < NBP; ++j) {
-            if (j < g.nba) {
-              const float ce = ckl[nkj + k * g.nba + j];
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) G[r][e] += ((sv[e][r] >> (3 * j)) & 1u) ? ce : 0.f;
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) G[r][e] *= gv[r][e];
-        }
-        // rows 4*qd + r, chunk-local kappa kq*4 .. +4: three bf16 parts
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint32_t ph[2], pm[2], pl2[2];
-#pragma unroll
-          for (int e2 = 0; e2 < 2; ++e2) {
-            const float a0 = G[r][2 * e2], a1 = G[r][2 * e2 + 1];
-            const __bf16 h0 = (__bf16)a0, h1 = (__bf16)a1;
-            const float s0 = a0 - (float)h0, s1 = a1 - (float)h1;
-            const __bf16 m0b = (__bf16)s0, m1b = (__bf16)s1;
-            const __bf16 l0 = (__bf16)(s0 - (float)m0b), l1 = (__bf16)(s1 - (float)m1b);
-            ph[e2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-            pm[e2] = (uint32_t)__builtin_bit_cast(uint16_t, m0b) | ((uint32_t)__builtin_bit_cast(uint16_t, m1b) << 16);
-            pl2[e2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-          }
-          const int off = (4 * qd + r) * GP + kq * 4;
-          *reinterpret_cast<uint2*>(Gs + off) = make_uint2(ph[0], ph[1]);
-          *reinterpret_cast<uint2*>(Gs + PART + off) = make_uint2(pm[0], pm[1]);
-          *reinterpret_cast<uint2*>(Gs + 2 * PART + off) = make_uint2(pl2[0], pl2[1]);
-        }
-      }
-      __syncthreads();
-      // phase B: every owned output tile, every tap
-#pragma unroll
-      for (int u = 0; u < TPW; ++u) {
-        const int t = wave + NW * u;
-        const int qb = t / v.CB, cb = t - qb * v.CB;
-        if (t < NTb && cb * 16 <= ci1 && cb * 16 + 15 >= ci0) {
-          v4f a = acc[u];
-#pragma unroll
-          for (int kh = 0; kh < KX; ++kh) {
-#pragma unroll
-            for (int kw = 0; kw < KX; ++kw) {
-              if (kh < g.KH && kw < g.KW) {
-                int row;
-                if constexpr (TPW <= 2) row = rowidx[(u * KX + kh) * KX + kw];
-                else row = grow_of(u, kh, kw);
-                const int khw = kh * g.KW + kw;
-                const v8bf gh = *reinterpret_cast<const v8bf*>(Gs + row * GP + 8 * g4);
-                const v8bf gm = *reinterpret_cast<const v8bf*>(Gs + PART + row * GP + 8 * g4);
-                const v8bf gl = *reinterpret_cast<const v8bf*>(Gs + 2 * PART + row * GP + 8 * g4);
-                const v8bf wv = *reinterpret_cast<const v8bf*>(Wb + (khw * Cp + cb * 16 + r16) * WPB + 8 * g4);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gh, wv, a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gm, wv, a, 0, 0, 0);
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gl, wv, a, 0, 0, 0);
-              }
-            }
-          }
-          acc[u] = a;
-        }
-      }
-    }
-  }
-  // epilogue from registers: acc[u][r] = gx_raw[q = qb*16 + 4*g4 + r, c = cb*16 + r16]
-  const float scale = sw / (float)g.nba;
-  float part = 0.f;
-#pragma unroll
-  for (int u = 0; u < TPW; ++u) {
-    const int t = wave + NW * u;
-    const int qb = t / v.CB, cb = t - qb * v.CB;
-    const int c = cb * 16 + r16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qa = qb * 16 + 4 * g4 + r;
-      if (t < NTb && qa < nq && c < g.C) {
-        const size_t gi = (((size_t)b * g.C + c) * g.H + r0) * g.W + qa;
-        const float gqv = acc[u][r] * scale;
-        if (LSQ) {
-          // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549)
-          const float xv = xpre[u][r];
-          const float y1 = xv / sa;
-          const float cl = clamp_nan(y1, 0.f, g.lsq_qp);
-          const float rr2 = rintf(cl);
-          const float rp = (rr2 - cl) + cl;
-          const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
-          const float gy = pass ? gqv * sa : 0.f;
-          gx[gi] = gy / sa;
-          part += gqv * rp;
-          part += -(gy * (y1 / sa));
-        } else {
-          gx[gi] = gqv;
-        }
-      }
-    }
-  }
-  if (LSQ) {
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-    if (lane == 0) red[wave] = part;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float sacc = 0.f;
-      for (int w = 0; w < NW; ++w) sacc += red[w];
-      gsa_part[blockIdx.x] = sacc;
-    }
-  }
-}
-
-// One grad_w pixel tile in one round of loads: forward slice rows (-> patch) and backward
-// slice rows (-> patchB, widened to bf16) of channels [c0, c0 + ncx) -- the channels tile i
-// touches.  Every thread issues up to 4 + 4 16-byte loads before its first LDS store.
-template <int NBP>
-__device__ inline void stage_gw_mtile(const Geo& g, int WP, int RHx, const uint8_t* __restrict__ xcf,
-                                      const uint8_t* __restrict__ xcb, int b, int ih_first, int c0, int ncx,
-                                      uint8_t* patch, uint8_t* patchB) {
-  const int QW = g.W * NBP / 16;
-  const int n = ncx * RHx * QW;
-  const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
-  const size_t img = ((size_t)b * g.C + c0) * g.H * QW;
-  const uint4* sf = reinterpret_cast<const uint4*>(xcf) + img;
-  const uint4* sb = reinterpret_cast<const uint4*>(xcb) + img;
-  const int nt = blockDim.x;
-  for (int base = threadIdx.x; base < n; base += 4 * nt) {
-    uint4 vf[4], vb[4];
-    int d[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = base + u * nt;
-      d[u] = -1;
-      if (idx < n) {
-        const int row = fdiv(idx, QW, invQ), q = idx - row * QW;
-        const int c = fdiv(row, RHx, invR), rr = row - c * RHx;
-        const int ih = ih_first + rr;
-        d[u] = ((c * RHx + rr) * WP + g.PW) * NBP + q * 16;
-        vf[u] = make_uint4(0, 0, 0, 0);
-        vb[u] = make_uint4(0, 0, 0, 0);
-        if (ih >= 0 && ih < g.H) {
-          const size_t si = ((size_t)c * g.H + ih) * QW + q;
-          vf[u] = sf[si];
-          vb[u] = sb[si];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (d[u] >= 0) {
-        uint32_t* pf = reinterpret_cast<uint32_t*>(patch + d[u]);
-        pf[0] = vf[u].x; pf[1] = vf[u].y; pf[2] = vf[u].z; pf[3] = vf[u].w;
-        uint32_t* pb = reinterpret_cast<uint32_t*>(patchB + 2 * d[u]);
-        const uint32_t w[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pb[2 * e] = bf16x2_of_bytes(w[e], 0);
-          pb[2 * e + 1] = bf16x2_of_bytes(w[e], 16);
-        }
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// grad_w + grad_alpha (and the alpha_cim init sums): block = (pixel chunk, tile i, 32 cols)
-//   D_j[m, o] = sum_k cD_kj * STE_ijk[m, o]
-//   gw_i[f, o] += sum_{j, m} xhat_j[m, f] * (g[m, o] * D_j[m, o])     (bf16x3 MFMA)
-//   ga[i, k, j, o] += sum_m code_ijk[m, o] * g[m, o]                   (lsq.py:257-333)
-// Only the input channels of tile i are staged; grad_out is read straight from memory, one
-// pixel tile ahead.
-// ---------------------------------------------------------------------------------------
-template <int NBP, int KS, int FBX, bool INIT>
-__global__ __launch_bounds__(256) void cim_bwd_gw_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
-                                                            const uint8_t* __restrict__ xcb,
-                                                            const v4i* __restrict__ wfrag, Params pp,
-                                                            const float* __restrict__ sw_p,
-                                                            const float* __restrict__ sa_p,
-                                                            const float* __restrict__ gout, int rows_per_chunk,
-                                                            float* __restrict__ gw_slab,
-                                                            float* __restrict__ ga_slab) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int nkj = g.nbw * g.nba;
-  const int i = blockIdx.y, og = blockIdx.z;
-  const int NOB = min(2, g.OB16);
-  const int nob = min(2, g.OB16 - og * 2);
-  const int c0 = (i * g.xbar) / g.KHW;
-  const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;
-  const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;  // f-blocks holding data in tile i
-  const int ncx = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW - c0 + 1;
-  const size_t pf = al16((size_t)v.NCG * v.RH * v.WP * NBP);
-  const size_t pbsz = INIT ? 0 : al16((size_t)v.NCG * v.RH * v.WP * NBP * 2);
-  const size_t gwsz = INIT ? 0 : (size_t)g.FBT * 16 * 32 * 4;
-
-  uint8_t* cur = smem;
-  uint8_t* patch = cur;
-  uint8_t* patchB = cur + pf;
-  float* gwacc = reinterpret_cast<float*>(cur);  // aliases the patches after the pixel loop
-  cur += max(pf + pbsz, gwsz);
-  int* ptab = reinterpret_cast<int*>(cur); cur += KS * 64 * 4;
-  v4i* wfl = reinterpret_cast<v4i*>(cur); cur += (size_t)g.nbw * NOB * KS * 1024;     // [k][ob][ks][64]
-  int4* prm = reinterpret_cast<int4*>(cur); cur += (size_t)nkj * NOB * 16 * 16;       // [j][k][NOB*16]
-  // INIT: one |u| partial-sum row per wave, summed in wave order at the end (no float
-  // atomics: the alpha_cim init is bit-reproducible, lsq.py:559-562)
-  float* qacc = reinterpret_cast<float*>(cur); cur += al16((size_t)nkj * 32 * 4 * (INIT ? 4 : 1));
-  float* ckl = reinterpret_cast<float*>(cur);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const int mbeg = blockIdx.x * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
-  const float sw = *sw_p, sa = *sa_p;
-  const bool literal = (pp.flags[0] != 0);
-  const bool ternary_fast = (!literal) && g.mode == ADC_TERNARY;
-  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
-  const int Wo = 1 << v.lw;
-
-  for (int t = threadIdx.x; t < nkj * 32 * (INIT ? 4 : 1); t += blockDim.x) qacc[t] = 0.f;
-  for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
-  build_ptab(g, i, KS, v.RH, v.WP, ptab, c0);
-  batched_copy<4>(g.nbw * NOB * KS * 64, wfl, [&](int idx) -> v4i {
-    const int l = idx & 63, fr = idx >> 6;
-    const int ks = fr % KS, kob = fr / KS, k = kob / NOB, ob = kob - k * NOB;
-    v4i w = {0, 0, 0, 0};
-    if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * 2 + ob) * WAVE + l];
-    return w;
-  });
-  batched_copy<2>(nkj * NOB * 16, prm, [&](int idx) -> int4 {
-    const int col = idx % (NOB * 16), jk = idx / (NOB * 16), k = jk % g.nbw, j = jk / g.nbw;
-    const int o = og * 32 + col;
-    int4 p = make_int4(0, 0, 0, 0);
-    if (o < g.Opad) {
-      const int pi = pidx(g, i, j, k, o);
-      p = make_int4(pp.mlo[pi], pp.mhi[pi], pp.thi[pi], pp.tlo[pi]);
-    }
-    return p;
-  });
-  zero_lds(reinterpret_cast<uint32_t*>(patch), (int)((pf + pbsz) / 4));
-  __syncthreads();
-
-  // gather column pixel (i8 operand) and this lane's 4 accumulator-row pixels
-  const int pl = wave * 16 + r16;
-  const int rb = ((pl >> v.lw) * g.SH) * v.WP + (pl & (Wo - 1)) * g.SW;
-  int rb4[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = wave * 16 + 4 * g4 + r;
-    rb4[r] = ((q >> v.lw) * g.SH) * v.WP + (q & (Wo - 1)) * g.SW;
-  }
-  int ptf[FBX];
-#pragma unroll
-  for (int fb = 0; fb < FBX; ++fb) ptf[fb] = (fb < g.FBT) ? ptab[fb * 16 + r16] : 0;
-
-  // grad_out of this lane's accumulator rows (4 pixels) for its column in each o-block
-  auto load_gv = [&](int m0, float (&dst)[2][4]) {
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob) {
-      const int o = og * 32 + ob * 16 + r16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dst[ob][r] = 0.f;
-        if (!INIT && m0 < mend && ob < nob && o < g.O)
-          dst[ob][r] = gout[(size_t)(m0 + wave * 16 + 4 * g4 + r) * g.O + o];
-      }
-    }
-  };
-  float gnext[2][4];
-  load_gv(mbeg, gnext);
-
-  v4f gwa[FBX][2];
-#pragma unroll
-  for (int a = 0; a < FBX; ++a) {
-    gwa[a][0] = v4f{0.f, 0.f, 0.f, 0.f};
-    gwa[a][1] = v4f{0.f, 0.f, 0.f, 0.f};
-  }
-  const int tiles_per_img = g.P >> 6;
-
-  for (int m0 = mbeg; m0 < mend; m0 += 64) {
-    const int mt = m0 >> 6;
-    const int b = mt / tiles_per_img, p0 = (mt - b * tiles_per_img) * 64;
-    const int ih_first = (p0 >> v.lw) * g.SH - g.PH;
-    __syncthreads();
-    if (INIT) stage_rows<NBP>(g, v.WP, v.RH, xcf, b, ih_first, patch, c0, ncx);
-    else stage_gw_mtile<NBP>(g, v.WP, v.RH, xcf, xcb, b, ih_first, c0, ncx, patch, patchB);
-    float gcur[2][4];
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gcur[ob][r] = gnext[ob][r];
-    __syncthreads();
-    load_gv(m0 + 64, gnext);
-
-    v4i xs[NBP][KS];
-    gather_xs<NBP, KS>(patch, rb, ptab, g4, xs, ksn);
-#pragma unroll
-    for (int ob = 0; ob < 2; ++ob) {
-      if (ob < nob) {
-        const int ocol = ob * 16 + r16;
-        const float* gval = gcur[ob];
-        float D[NBP][4];
-#pragma unroll
-        for (int j = 0; j < NBP; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) D[j][r] = 0.f;
-        for (int k = 0; k < g.nbw; ++k) {
-          v4i wk[KS];
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) wk[ks] = wfl[((k * NOB + ob) * KS + ks) * 64 + lane];
-#pragma unroll
-          for (int j = 0; j < NBP; ++j) {
-            if (j < g.nba) {
-              v4i ps = {0, 0, 0, 0};
-#pragma unroll
-              for (int ks = 0; ks < KS; ++ks) if (ks < ksn) ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps, 0, 0, 0);
-              const int kj = k * g.nba + j;
-              float qs = 0.f;
-              if (INIT) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) qs += fabsf(((float)ps[r] * sw) * sa);  // lsq.py:64,84
-              } else {
-                const float cd = ckl[2 * nkj + kj];
-                const int4 pv = prm[(j * g.nbw + k) * NOB * 16 + ocol];
-                if (ternary_fast) {
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) {
-                    const int p = ps[r];
-                    D[j][r] += ((unsigned)(p - pv.x) <= (unsigned)pv.y) ? cd : 0.f;
-                    float q = (p >= pv.z) ? gval[r] : 0.f;
-                    q = (p <= pv.w) ? -gval[r] : q;
-                    qs += q;
-                  }
-                } else {
-                  const int o = og * 32 + ocol;
-                  const float al = pp.alpha[pidx(g, i, j, k, o)];
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) {
-                    const int p = ps[r];
-                    const bool pass = literal ? (ste_literal(p, g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f)
-                                              : ((unsigned)(p - pv.x) <= (unsigned)pv.y);
-                    D[j][r] += pass ? cd : 0.f;
-                    if (has_code) qs += code_literal(p, g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo) * gval[r];
-                  }
-                }
-              }
-              if (INIT || has_code) {
-                qs += __shfl_xor(qs, 16);
-                qs += __shfl_xor(qs, 32);
-                if (INIT) {
-                  if (g4 == 0) qacc[(wave * nkj + kj) * 32 + ocol] += qs;  // one writer per slot
-                } else if (g4 == 0) {
-                  atomicAdd(&qacc[kj * 32 + ocol], qs);
-                }
-              }
-            }
-          }
-        }
-        if (!INIT) {
-          // B operands (k = (j-pair half h2, pixel r)) for every j-pair, then the f-blocks
-          constexpr int NS = NBP / 2;
-          v8bf bh[NS], bm[NS], bl[NS];
-#pragma unroll
-          for (int s2 = 0; s2 < NS; ++s2) {
-            float ev[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int j = 2 * s2 + (e >> 2), r = e & 3;
-              ev[e] = (j < g.nba) ? gval[r] * D[j][r] : 0.f;
-            }
-            split3x8(ev, bh[s2], bm[s2], bl[s2]);
-          }
-          const uint32_t* pB = reinterpret_cast<const uint32_t*>(patchB);
-#pragma unroll
-          for (int fb = 0; fb < FBX; ++fb) {
-            if (fb < fbn) {
-              v4f accw = gwa[fb][ob];
-#pragma unroll
-              for (int s2 = 0; s2 < NS; ++s2) {
-                if (2 * s2 < g.nba) {
-                  uint32_t d[4];
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) d[r] = pB[(rb4[r] + ptf[fb]) * NS + s2];
-                  v4i a;
-                  a[0] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x05040100u);
-                  a[1] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x05040100u);
-                  a[2] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
-                  a[3] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
-                  const v8bf xa = as_v8bf(a);
-                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bh[s2], accw, 0, 0, 0);
-                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bm[s2], accw, 0, 0, 0);
-                  accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bl[s2], accw, 0, 0, 0);
-                }
-              }
-              gwa[fb][ob] = accw;
-            }
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (!INIT) {
-    for (int t = threadIdx.x; t < g.FBT * 16 * 32; t += blockDim.x) gwacc[t] = 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int fb = 0; fb < FBX; ++fb)
-      if (fb < g.FBT)
-#pragma unroll
-        for (int ob = 0; ob < 2; ++ob)
-          if (ob < nob)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * 32 + ob * 16 + r16], gwa[fb][ob][r]);
-    __syncthreads();
-  }
-  const int mc = blockIdx.x;
-  for (int t = threadIdx.x; t < nkj * 32; t += blockDim.x) {
-    const int q = t >> 5, col = t & 31;
-    const int o = og * 32 + col;
-    float qv = qacc[t];
-    if (INIT) qv = ((qv + qacc[nkj * 32 + t]) + qacc[2 * nkj * 32 + t]) + qacc[3 * nkj * 32 + t];
-    if (o < g.Opad) ga_slab[(((size_t)mc * g.T + i) * nkj + q) * g.Opad + o] = qv;
-  }
-  if (INIT) return;
-  for (int t = threadIdx.x; t < g.FBT * 16 * 32; t += blockDim.x) {
-    const int fl = t >> 5, col = t & 31;
-    const int o = og * 32 + col;
-    if (o < g.Opad) gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o] = gwacc[t];
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// grad_w from the forward's state words: block = (pixel chunk, tile i, 32 output channels);
-//   D_j[m, o] = sum_k cD_kj * STE_ijk[m, o]
-//   gw_i[f, o] += sum_{j, m} xhat_j[m, f] * (g[m, o] * D_j[m, o])     (bf16x3 MFMA)
-// Only the input channels of tile i are staged (as bf16 backward slices); grad_out and the
-// state words are read straight from memory, one pixel tile ahead.
-// ---------------------------------------------------------------------------------------
-template <int NBP, int FBX, int NBWX>
-__global__ __launch_bounds__(256, 1) void cim_bwd_gw_v5_kernel(Geo g, V3 v, const uint8_t* __restrict__ st,
-                                                               const uint8_t* __restrict__ xcb, Params pp,
-                                                               const float* __restrict__ gout, int rows_per_chunk,
-                                                               float* __restrict__ gw_slab, float* __restrict__ ga_slab) {
-  constexpr int NS = NBP / 2;
-  constexpr int SWD = NBP / 2;  // state dwords per (pixel quad, channel): 4 x uint16 or 4 x uint32
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int nkj = g.nbw * g.nba;
-  const int i = blockIdx.y, ob = blockIdx.z;  // one 16-channel block
-  const int c0 = (i * g.xbar) / g.KHW;
-  const int fbn = (min(g.xbar, g.K - i * g.xbar) + 15) >> 4;  // f-blocks holding data in tile i
-  const int ncx = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW - c0 + 1;
-  const size_t pbsz = al16((size_t)v.NCG * v.RH * v.WP * NBP * 2);
-  const size_t gwsz = (size_t)g.FBT * 16 * 16 * 4;
-
-  uint8_t* cur = smem;
-  uint8_t* patchB = cur;
-  float* gwacc = reinterpret_cast<float*>(cur);  // aliases the patch after the pixel loop
-  cur += max(pbsz, gwsz);
-  int* ptab = reinterpret_cast<int*>(cur); cur += 128 * 4;
-  float* qacc = reinterpret_cast<float*>(cur); cur += al16((size_t)nkj * 16 * 4);  // [kj][16 channels]
-  float* ckl = reinterpret_cast<float*>(cur);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r16 = lane & 15, g4 = lane >> 4;
-  const int mbeg = blockIdx.x * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
-  const int Wo = 1 << v.lw;
-  const size_t MQ = (size_t)g.M >> 2;
-  const int o = ob * 16 + r16;
-  const bool ocol = o < g.O;
-
-  for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
-  for (int t = threadIdx.x; t < nkj * 16; t += blockDim.x) qacc[t] = 0.f;
-  const bool has_code = (g.mode == ADC_SIGN || g.mode == ADC_TERNARY);
-  build_ptab(g, i, 2, v.RH, v.WP, ptab, c0);
-  zero_lds(reinterpret_cast<uint32_t*>(patchB), (int)(pbsz / 4));
-  __syncthreads();
-
-  // this lane's 4 accumulator-row pixels (B-operand k-values) and its f-row per f-block
-  int rb4[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = wave * 16 + 4 * g4 + r;
-    rb4[r] = ((q >> v.lw) * g.SH) * v.WP + (q & (Wo - 1)) * g.SW;
-  }
-  int ptf[FBX];
-#pragma unroll
-  for (int fb = 0; fb < FBX; ++fb) ptf[fb] = (fb < g.FBT) ? ptab[fb * 16 + r16] : 0;
-
-  // grad_out and raw state dwords of this lane's 4 pixels, channel o
-  auto load_in = [&](int m0, float (&gd)[4], uint32_t (&sd)[NBWX][SWD]) {
-    const bool ok = m0 < mend && ocol;
-    const size_t mq = ((size_t)m0 >> 2) + wave * 4 + g4;
-    const float4 g4v = ok ? load_g4(g, gout, (size_t)m0 + wave * 16 + 4 * g4, o) : make_float4(0.f, 0.f, 0.f, 0.f);
-    gd[0] = g4v.x; gd[1] = g4v.y; gd[2] = g4v.z; gd[3] = g4v.w;
-#pragma unroll
-    for (int k = 0; k < NBWX; ++k) {
-#pragma unroll
-      for (int d = 0; d < SWD; ++d) sd[k][d] = 0u;
-      if (k < g.nbw && ok) {
-        const size_t q = ((size_t)(i * g.nbw + k) * MQ + mq) * g.O + o;
-        if (SWD == 2) {
-          const uint2 w = reinterpret_cast<const uint2*>(st)[q];
-          sd[k][0] = w.x; sd[k][1] = w.y;
-        } else {
-          const uint4 w = reinterpret_cast<const uint4*>(st)[q];
-          sd[k][0] = w.x; sd[k][1] = w.y;
-          if (SWD == 4) { sd[k][SWD - 2] = w.z; sd[k][SWD - 1] = w.w; }
-        }
-      }
-    }
-  };
-  auto word = [&](const uint32_t (&sd)[NBWX][SWD], int k, int r) -> uint32_t {
-    if (SWD == 2) return (sd[k][r >> 1] >> (16 * (r & 1))) & 0xFFFFu;
-    return sd[k][r];
-  };
-  float gnext[4];
-  uint32_t snext[NBWX][SWD];
-  load_in(mbeg, gnext, snext);
-
-  v4f gwa[FBX];
-#pragma unroll
-  for (int a = 0; a < FBX; ++a) gwa[a] = v4f{0.f, 0.f, 0.f, 0.f};
-  // grad_alpha_cim partial sums (lsq.py:321-333): sum over this lane's pixels of code * g
-  float qs[NBWX][NBP];
-#pragma unroll
-  for (int kk = 0; kk < NBWX; ++kk)
-#pragma unroll
-    for (int j = 0; j < NBP; ++j) qs[kk][j] = 0.f;
-  const int tiles_per_img = g.P >> 6;
-
-  for (int m0 = mbeg; m0 < mend; m0 += 64) {
-    const int mt = m0 >> 6;
-    const int b = mt / tiles_per_img, p0 = (mt - b * tiles_per_img) * 64;
-    const int ih_first = (p0 >> v.lw) * g.SH - g.PH;
-    __syncthreads();
-    stage_rows_bf16<NBP>(g, v.WP, v.RH, xcb, b, ih_first, patchB, c0, ncx);
-    float gcur[4];
-    uint32_t scur[NBWX][SWD];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gcur[r] = gnext[r];
-#pragma unroll
-    for (int k = 0; k < NBWX; ++k)
-#pragma unroll
-      for (int d = 0; d < SWD; ++d) scur[k][d] = snext[k][d];
-    __syncthreads();
-    load_in(m0 + 64, gnext, snext);
-
-    float D[NBP][4];
-#pragma unroll
-    for (int j = 0; j < NBP; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) D[j][r] = 0.f;
-#pragma unroll
-    for (int k = 0; k < NBWX; ++k) {
-      if (k < g.nbw) {
-#pragma unroll
-        for (int j = 0; j < NBP; ++j) {
-          if (j < g.nba) {
-            const float cd = ckl[2 * nkj + k * g.nba + j];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t bits = word(scur, k, r) >> (3 * j);
-              D[j][r] += (bits & 1u) ? cd : 0.f;
-              qs[k][j] += (bits & 2u) ? ((bits & 4u) ? -gcur[r] : gcur[r]) : 0.f;
-            }
-          }
-        }
-      }
-    }
-    // B operands (k = (j-pair half h2, pixel r)) for every j-pair, then the f-blocks
-    v8bf bh[NS], bm[NS], bl[NS];
-#pragma unroll
-    for (int s2 = 0; s2 < NS; ++s2) {
-      float ev[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int j = 2 * s2 + (e >> 2), r = e & 3;
-        ev[e] = (j < g.nba) ? gcur[r] * D[j][r] : 0.f;
-      }
-      split3x8(ev, bh[s2], bm[s2], bl[s2]);
-    }
-    const uint32_t* pB = reinterpret_cast<const uint32_t*>(patchB);
-#pragma unroll
-    for (int fb = 0; fb < FBX; ++fb) {
-      if (fb < fbn) {
-        v4f accw = gwa[fb];
-#pragma unroll
-        for (int s2 = 0; s2 < NS; ++s2) {
-          if (2 * s2 < g.nba) {
-            uint32_t d[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) d[r] = pB[(rb4[r] + ptf[fb]) * NS + s2];
-            v4i a;
-            a[0] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x05040100u);
-            a[1] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x05040100u);
-            a[2] = (int)__builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
-            a[3] = (int)__builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
-            const v8bf xa = as_v8bf(a);
-            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bh[s2], accw, 0, 0, 0);
-            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bm[s2], accw, 0, 0, 0);
-            accw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, bl[s2], accw, 0, 0, 0);
-          }
-        }
-        gwa[fb] = accw;
-      }
-    }
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < g.FBT * 16 * 16; t += blockDim.x) gwacc[t] = 0.f;
-  __syncthreads();
-#pragma unroll
-  for (int fb = 0; fb < FBX; ++fb)
-    if (fb < g.FBT)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&gwacc[(fb * 16 + 4 * g4 + r) * 16 + r16], gwa[fb][r]);
-  __syncthreads();
-  const int mc = blockIdx.x;
-  if (has_code) {
-#pragma unroll
-    for (int kk = 0; kk < NBWX; ++kk) {
-#pragma unroll
-      for (int j = 0; j < NBP; ++j) {
-        if (kk < g.nbw && j < g.nba) {
-          float q = qs[kk][j];
-          q += __shfl_xor(q, 16);
-          q += __shfl_xor(q, 32);
-          if (g4 == 0) atomicAdd(&qacc[(kk * g.nba + j) * 16 + r16], q);
-        }
-      }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < nkj * 16; t += blockDim.x) {
-      const int kj = t >> 4, col = t & 15;
-      ga_slab[(((size_t)mc * g.T + i) * nkj + kj) * g.Opad + ob * 16 + col] = qacc[t];
-    }
-  }
-  for (int t = threadIdx.x; t < g.FBT * 16 * 16; t += blockDim.x) {
-    const int fl = t >> 4, col = t & 15;
-    const int oo = ob * 16 + col;
-    gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + oo] = gwacc[t];
   }
 }
 

@@ -202,16 +202,6 @@ StatsKernel stats_ptr() {
   return shift_stats_kernel<KS, NS, LUT>;
 }
 
-// half-range of the q tables: the largest |ps| of 0 .. 2^bs - 1 slices over one tile (the sign slice of
-// the weights included); larger partial sums (slice artifacts) take the direct evaluation
-inline int shift_table_range(const Geo& g) {
-  const int tmax = std::min(g.K, g.xbar);
-  return tmax * ((1 << g.bsa) - 1) * ((1 << g.bsw) - 1);
-}
-inline bool shift_table_fits(const Geo& g) {
-  return (size_t)g.nbw * g.nba * 16 * (2 * shift_table_range(g) + 1) * 4 <= 48 * 1024;
-}
-
 int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
                        const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s,
                        int accum_beta) {

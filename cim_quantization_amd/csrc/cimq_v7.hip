@@ -28,7 +28,7 @@
 #pragma once
 #include <type_traits>
 
-#include "cimq_gx_v6.hip"
+#include "cimq_kernels_v3.hip"
 #include "cimq_lsq_dev.h"
 
 namespace cimq {
