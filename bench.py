@@ -39,10 +39,12 @@ XBAR, ADC = 128, 1.5
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward runs bf16 x3
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
-TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r03_final", "pmc_traffic.json"))
-# rocprof symbol of each v7-path kernel id (the names pmc_traffic.json is keyed by)
-V7_SYMBOLS = {"fwd_v7": "cimq::cim_fwd_v3_kernel<4, 2, 3, ", "gx_v8": "cimq::cim_bwd_gx_v8_kernel<3, 3, ",
-              "gw_v7": "cimq::cim_bwd_gw_v7_kernel<3, 3>"}
+PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD-32 x 2.4 GHz (a wave64 VALU op issues over 2 cycles)
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r04", "pmc_traffic.json"))
+# the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
+# prefixes (the keys of pmc_traffic.json); every launch of a family is timed, all its instantiations
+FAMILIES = {"fwd_v7": "cimq::cim_fwd_v3_kernel<", "bwd_fused": "cimq::cim_bwd_fused_kernel<",
+            "gx_v8": "cimq::cim_bwd_gx_v8_kernel<", "gw_v7": "cimq::cim_bwd_gw_v7_kernel<"}
 
 
 def out_hw(h, s):
@@ -194,20 +196,69 @@ def timed_forward(trainer, xs, steps, dev, world, graph):
     return time.perf_counter() - t0
 
 
+def live_pairs(nb):
+    """slice pairs with a nonzero int8 binary_mask entry (2^(j+k) wraps to 0 at >= 2^8, _quan_base.py:207-214)."""
+    return sum(1 for k in range(nb) for j in range(nb) if j + k <= 7)
+
+
 def step_context(batch, world, ms_step, ms_fwd):
-    """SURVEY 8(d) / BASELINE.md rates of the 19 layers: bit-sliced MAC/s of the forward (logical MAC x
-    nbw x nba, the products the crossbar model computes) and algorithmic HBM GB/s of fwd+bwd (per layer
-    forward 4(|x|+|y|), grad_x 8|x|+4|y|, grad_w 4(|x|+|y|) bytes)."""
+    """SURVEY 8(d) / BASELINE.md rates of the 19 layers: bit-sliced MAC/s of the forward (logical MAC x the
+    live slice pairs, the products the crossbar model computes), algorithmic HBM GB/s of fwd+bwd (per layer
+    12 B per input element + 8 B per output element: the forward reads x and writes y, the backward reads
+    grad_y and x and writes grad_x -- 961.5 MB per step at B = 256) and the step's own roofs: HBM on those
+    bytes, MFMA on the forward's int8 bit-slice products plus the backward's fp32-accurate contraction as
+    three bf16 products."""
     bs_mac = 0.0
     byts = 0.0
+    t_i8 = t_bf = 0.0
     for _, c, o, h, s, nb in RESNET20:
         ho = out_hw(h, s)
-        bs_mac += batch * ho * ho * o * c * 9 * nb * nb
+        mac = batch * ho * ho * o * c * 9
+        bs_mac += mac * live_pairs(nb)
         nx, ny = batch * c * h * h, batch * o * ho * ho
-        byts += 16.0 * nx + 12.0 * ny
+        byts += 12.0 * nx + 8.0 * ny
+        t_i8 += 2.0 * mac * live_pairs(nb) / (PEAK_I8_TOPS * 1e12)
+        t_bf += 3.0 * 2.0 * mac * (nb + nb) / (PEAK_BF16_TFLOPS * 1e12)
+    t_hbm = byts / (PEAK_HBM_GBS * 1e9)
     return {"bit_sliced_mac_per_s_fwd": bs_mac * world / (ms_fwd * 1e-3),
             "algorithmic_hbm_gb_per_s_fwd_bwd": byts * world / (ms_step * 1e-3) / 1e9,
-            "algorithmic_bytes_per_step_per_gpu": byts}
+            "algorithmic_bytes_per_step_per_gpu": byts,
+            "step_roofline": {"t_hbm_us": t_hbm * 1e6, "t_mfma_us": (t_i8 + t_bf) * 1e6,
+                              "t_mfma_fwd_i8_us": t_i8 * 1e6, "t_mfma_bwd_bf16x3_us": t_bf * 1e6,
+                              "frac_hbm": t_hbm / (ms_step * 1e-3), "frac_mfma": (t_i8 + t_bf) / (ms_step * 1e-3)}}
+
+
+def family_roofline(kt, family, steps):
+    """Roofline of one kernel family from its per-launch HIP-event times (cimq_profile_read): each launch
+    is bounded by t_roof = max(t_HBM, t_MFMA) of its own algorithmic bytes and MFMA operations (int8 at
+    5 POP/s forward, bf16 at 2.5 PFLOP/s backward); frac = sum t_roof / sum t_measured over the family.
+    achieved = frac x the peak of the roof that binds most of the family's t_roof."""
+    peak_m = PEAK_I8_TOPS if family == "fwd_v7" else PEAK_BF16_TFLOPS
+    pl = kt.per_launch
+    tm = sum(ms for ms, _, _, _ in pl) * 1e-3
+    roof_h = roof_m = 0.0
+    classes = {}
+    for ms, byts, _, mops in pl:
+        th, tmf = byts / (PEAK_HBM_GBS * 1e9), mops / (peak_m * 1e12)
+        if th >= tmf:
+            roof_h += th
+        else:
+            roof_m += tmf
+        c = classes.setdefault((round(byts), round(mops)), [0, 0.0, th, tmf])
+        c[0] += 1
+        c[1] += ms * 1e-3
+    frac = (roof_h + roof_m) / tm
+    bound = "hbm" if roof_h >= roof_m else "mfma"
+    peak = PEAK_HBM_GBS if bound == "hbm" else peak_m
+    unit = "GB/s" if bound == "hbm" else ("TOP/s" if family == "fwd_v7" else "TFLOP/s")
+    inst = [{"launches": n, "algo_bytes": b, "mfma_ops": m, "t_hbm_us": th * 1e6, "t_mfma_us": tmf * 1e6,
+             "avg_launch_us": t / n * 1e6, "frac": max(th, tmf) / (t / n)}
+            for (b, m), (n, t, th, tmf) in sorted(classes.items(), key=lambda kv: -kv[1][1])]
+    return {"bound": bound, "achieved": frac * peak, "peak": peak, "unit": unit, "frac": frac,
+            "family_us_per_step": tm / steps * 1e6, "t_roof_us_per_step": (roof_h + roof_m) / steps * 1e6,
+            "launches": len(pl), "instances": inst,
+            "method": "frac = sum_i max(t_hbm_i, t_mfma_i) / sum_i t_i over every launch i of the family "
+                      "(HIP events on the launch stream); achieved = frac x peak of the binding roof"}
 
 
 def measured_peaks(dev):
@@ -253,20 +304,26 @@ def source_sha():
     return h.hexdigest()[:16]
 
 
-def measured_traffic(dominant):
-    """Launch-weighted HBM bytes per launch of the dominant kernel family from the committed
-    PMC passes (tools/pmc_traffic.py), or (None, reason) when they measured other sources."""
+def measured_pmc(family):
+    """Launch-weighted HBM bytes (2 FETCH_SIZE + WRITE_SIZE) and VALU instructions per launch of a kernel
+    family from the committed PMC passes (tools/pmc_traffic.py), or None with the reason when those
+    passes measured other kernel sources."""
     if not os.path.exists(TRAFFIC_JSON):
-        return None, "no PMC traffic file"
+        return None, None, "no PMC file"
     tj = json.load(open(TRAFFIC_JSON))
     meta = tj.pop("_meta", {})
+    src = os.path.relpath(TRAFFIC_JSON, REPO)
     if meta.get("source_sha") != source_sha():
-        return None, f"{os.path.relpath(TRAFFIC_JSON, REPO)} measured other kernel sources"
-    hits = [(v["traffic_bytes"], v.get("dispatches", 1)) for k, v in tj.items() if k.startswith(V7_SYMBOLS[dominant])]
+        return None, None, f"{src} measured other kernel sources"
+    hits = [v for k, v in tj.items() if k.startswith(FAMILIES[family])]
     if not hits:
-        return None, "dominant kernel absent from the PMC file"
-    n = sum(c for _, c in hits)
-    return sum(b * c for b, c in hits) / n, os.path.relpath(TRAFFIC_JSON, REPO)
+        return None, None, "family absent from the PMC file"
+    n = sum(v.get("dispatches", 1) for v in hits)
+    traffic = sum(v["traffic_bytes"] * v.get("dispatches", 1) for v in hits) / n
+    valu = None
+    if all(v.get("valu_insts") is not None for v in hits):
+        valu = sum(v["valu_insts"] * v.get("dispatches", 1) for v in hits) / n
+    return traffic, valu, src
 
 
 def layer_breakdown(trainer, xs, gs, dev):
@@ -495,20 +552,20 @@ def main():
         tr.step(xs, gs)
     torch.cuda.synchronize(dev)
 
-    # per-role kernel ms of one untimed step (all variants), and the dominant v7-path kernel
+    # per-role kernel ms of one untimed step (all variants), and the dominant kernel family
     per_kernel = {}
-    for kname in ("fwd", "bwd_gx", "bwd_gw", "prep_act", "fwd_v7", "gx_v8", "gw_v7"):
+    for kname in ("fwd", "bwd_gx", "bwd_gw", "prep_act") + tuple(FAMILIES):
         with _lib.KernelTimer(kname) as kt:
             tr.step(xs, gs)
         per_kernel[kname] = kt.total_ms
-    dominant = max(("fwd_v7", "gx_v8", "gw_v7"), key=per_kernel.get)
+    dominant = max(FAMILIES, key=per_kernel.get)
 
     graph = not args.no_graph
     if graph:
         tr.flat.zero_()
         tr.capture(xs, gs)
         elapsed = timed(tr, xs, gs, args.steps, dev, world, True)
-        # HIP events recorded inside a graph cannot be timed on ROCm 7: the dominant kernel's
+        # HIP events recorded inside a graph cannot be timed on ROCm 7: the dominant family's
         # launches are timed over the same number of host-launched steps right after (same
         # inputs, same kernels; only the launch path differs)
         with _lib.KernelTimer(dominant, max_launches=len(RESNET20) * args.steps + 8) as kt:
@@ -528,25 +585,18 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     macs_step = macs_per_sample() * args.batch * world
     value = macs_step / (elapsed / args.steps)
+    roof = family_roofline(kt, dominant, args.steps)
     nl = max(kt.launches, 1)
-    avg_launch_ms = kt.total_ms / nl
-    bytes_l, flops_l = kt.algo_bytes / nl, kt.algo_flops / nl
-    # both roofs of the kernel: HBM on the algorithmic bytes; MFMA on the
-    # algorithmic products as the kernel issues them (backward: fp32-accurate = 3 bf16 MFMAs;
-    # forward: nbw*nba = 9 int8 bit-slice products per logical MAC)
-    t_hbm = bytes_l / (PEAK_HBM_GBS * 1e9)
-    mfma_ops = flops_l * (9.0 if dominant == "fwd_v7" else 3.0)
-    mfma_peak = PEAK_I8_TOPS if dominant == "fwd_v7" else PEAK_BF16_TFLOPS
-    t_mfma = mfma_ops / (mfma_peak * 1e12)
-    traffic, traffic_source = measured_traffic(dominant)
-    if t_hbm >= t_mfma:
-        roof = {"bound": "hbm", "achieved": bytes_l / (avg_launch_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
-                "unit": "GB/s"}
-    else:
-        roof = {"bound": "mfma", "achieved": mfma_ops / (avg_launch_ms * 1e-3) / 1e12, "peak": mfma_peak,
-                "unit": "TOP/s" if dominant == "fwd_v7" else "TFLOP/s"}
-    roof["frac"] = roof["achieved"] / roof["peak"]
+    traffic, valu, pmc_source = measured_pmc(dominant)
     roof["traffic"] = traffic
+    # VALU issue roof: the family's VALU instructions (PMC SQ_INSTS_VALU per launch) at one wave64
+    # instruction per 2 cycles per SIMD on every SIMD of the chip, against its measured time
+    if valu is not None:
+        t_valu = valu * 64.0 / PEAK_VALU_LANE_OPS
+        roof["valu"] = {"insts_per_launch": valu, "t_valu_us": t_valu * 1e6,
+                        "frac": t_valu / (kt.total_ms / nl * 1e-3), "peak_lane_ops_per_s": PEAK_VALU_LANE_OPS}
+    else:
+        roof["valu"] = None
     result = {
         "metric": "quantized-MAC/s + fwd+bwd ms per ResNet-20 w3a3 CiM layer, batch 256",
         "value": value,
@@ -569,11 +619,8 @@ def main():
                    "per_gpu_batch": args.batch, "xbar": XBAR, "adc_bits": ADC, "first_layer": "w8a8",
                    "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3),
                    "launch": "hip_graph" if graph else "eager"},
-        "roofline": dict(roof, kernel=_lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]],
-                         avg_launch_us=avg_launch_ms * 1e3, launches=kt.launches,
-                         algo_bytes_per_launch=bytes_l, algo_flops_per_launch=flops_l,
-                         t_hbm_us=t_hbm * 1e6, t_mfma_us=t_mfma * 1e6,
-                         traffic_source=traffic_source),
+        "roofline": dict(roof, kernel=_lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]] + " (every instantiation the "
+                         "19 layers launch)", avg_launch_us=kt.total_ms / nl * 1e3, pmc_source=pmc_source),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
         "rates": step_context(args.batch, world, ms_per_step, fwd_elapsed / args.steps * 1e3),

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -56,14 +56,15 @@ EXPORTED_SYMBOLS = (
     "cimq_qconv_backward_scales",
     "cimq_profile_start",
     "cimq_profile_stop",
+    "cimq_profile_read",
 )
 
-KERNEL_IDS = {"fwd": 1, "bwd_gx": 2, "bwd_gw": 3, "prep_act": 4, "fwd_v7": 5, "gx_v8": 6, "gw_v7": 7}
+KERNEL_IDS = {"fwd": 1, "bwd_gx": 2, "bwd_gw": 3, "prep_act": 4, "fwd_v7": 5, "gx_v8": 6, "gw_v7": 7, "bwd_fused": 8}
 # ids 1-4 time every launch of a role (all kernel variants); 5-7 only the v7-path kernels, one
 # rocprof symbol family each (the <NBW, NBA, ...> instantiation the workload uses)
 KERNEL_SYMBOLS = {1: "cim_fwd_*", 2: "cim_bwd_gx_*", 3: "cim_bwd_gw_*", 4: "prep_act_kernel",
-                  5: "cim_fwd_v3_kernel<4, 2, 3, *>", 6: "cim_bwd_gx_v8_kernel<3, 3, *, true>",
-                  7: "cim_bwd_gw_v7_kernel<3, 3>"}
+                  5: "cim_fwd_v3_kernel<*, *, *, *>", 6: "cim_bwd_gx_v8_kernel<*, *, *, *, *, *>",
+                  7: "cim_bwd_gw_v7_kernel<*, *, *>", 8: "cim_bwd_fused_kernel<*, *, *>"}
 
 
 class ConvDesc(ctypes.Structure):
@@ -196,6 +197,8 @@ def _bind(lib):
     lib.cimq_qconv_backward_scales.argtypes = [ctypes.POINTER(QConvDesc)] + [_VP] * 8
     lib.cimq_profile_start.restype = ctypes.c_int
     lib.cimq_profile_start.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.cimq_profile_read.restype = ctypes.c_int
+    lib.cimq_profile_read.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_double)] * 4 + [ctypes.POINTER(ctypes.c_int)]
     lib.cimq_profile_stop.restype = ctypes.c_int
     lib.cimq_profile_stop.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
@@ -300,6 +303,13 @@ class KernelTimer:
     def __exit__(self, *exc):
         ms, n = ctypes.c_double(), ctypes.c_int()
         b, f = ctypes.c_double(), ctypes.c_double()
+        # per launch (cimq_profile_read, ABI 9): duration, algorithmic bytes, logical flops, MFMA ops
+        cap = self.cap
+        arr = [(ctypes.c_double * cap)() for _ in range(4)]
+        got = ctypes.c_int()
+        check(load().cimq_profile_read(cap, *arr, ctypes.byref(got)), "cimq_profile_read")
+        k = min(cap, got.value)
+        self.per_launch = [tuple(a[i] for a in arr) for i in range(k)]
         check(load().cimq_profile_stop(ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), ctypes.byref(f)),
               "cimq_profile_stop")
         self.total_ms, self.launches = ms.value, n.value

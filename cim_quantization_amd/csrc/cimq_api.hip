@@ -69,6 +69,12 @@ static Carry no_carry() {
 int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                      const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused,
                      const Carry& carry = no_carry()) {
+  const Plan9 p9 = v9_plan(g);
+  if (p9.ok) {
+    const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
+    *lsq_fused = lsq;
+    return launch_fused(g, p9, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+  }
   const Plan7 p7 = v7_plan(g);
   if (p7.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
@@ -104,6 +110,16 @@ int launch_reduce_slab(const Geo& g, const uint8_t* ctx, uint8_t* ws, size_t sla
                      reinterpret_cast<const float*>(ws + slab), params_of(g, const_cast<uint8_t*>(ctx)), cgrad, 0,
                      sw, sa, 1.f, 1.f, out);
   return check_hip("reduce_slab");
+}
+
+// number of act-LSQ partials the backward leaves in ws (fused into the fused / v7 grad_x kernels,
+// else one per lsq_act_bwd_kernel block)
+int act_parts(const Geo& g) {
+  if (v9_plan(g).ok) return g.B;
+  const Plan7 p7 = v7_plan(g);
+  if (p7.ok) return g.B * p7.v.nbands;
+  int grid = cdiv(g.Nin, 256);
+  return grid > kLsqParts ? kLsqParts : grid;
 }
 
 }  // namespace
@@ -190,7 +206,7 @@ int cimq_shift_backward(const cimq_conv_desc* d, const float* grad_out, const fl
     CIMQ_TRY(launch_shift_stats(g, c, sw, sa, grad_out, binary_mask, w, grad_alpha, grad_beta, s));
     if (g.input_kind == CIMQ_INPUT_RAW_LSQ) {
       if (!lsq_fused) return fail(CIMQ_EINVAL, "internal: unfused act-LSQ backward on the v7 path");
-      hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, g.B * v7_plan(g).v.nbands,
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, act_parts(g),
                          reinterpret_cast<float*>(w + W.lsq_part), grad_sa);
       CIMQ_TRY(check_hip("sum_partials"));
     }
@@ -286,7 +302,7 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
     float* part = reinterpret_cast<float*>(w + W.lsq_part);
     int nparts;
     if (lsq_fused) {
-      nparts = g.B * v7_plan(g).v.nbands;
+      nparts = act_parts(g);
     } else {
       int grid = cdiv(g.Nin, 256);
       if (grid > kLsqParts) grid = kLsqParts;
@@ -298,15 +314,6 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
     CIMQ_TRY(check_hip("sum_partials"));
   }
   return CIMQ_OK;
-}
-
-// number of act-LSQ partials the backward leaves in ws (fused into the v7 grad_x kernel, else
-// one per lsq_act_bwd_kernel block)
-static int act_parts(const Geo& g) {
-  const Plan7 p7 = v7_plan(g);
-  if (p7.ok) return g.B * p7.v.nbands;
-  int grid = cdiv(g.Nin, 256);
-  return grid > kLsqParts ? kLsqParts : grid;
 }
 
 // the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes
@@ -584,7 +591,7 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
   if (lsq_fused) {
-    nparts = g.B * v7_plan(g).v.nbands;
+    nparts = act_parts(g);
   } else {
     int grid = cdiv(g.Nin, 256);
     if (grid > kLsqParts) grid = kLsqParts;
@@ -682,7 +689,7 @@ int cimq_module_shift_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
   g.onchw = 1;
   bool lsq_fused = false;
   CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, signed_act, grad_out, x, grad_x, w, s, &lsq_fused));
-  if (!lsq_fused || g.B * v7_plan(g).v.nbands != act_parts(g))
+  if (!lsq_fused)
     return fail(CIMQ_EINVAL, "internal: act-LSQ partials off the fused grad_x");
   // d loss / d alpha_q and grad_beta (scale_shift.py:488-501) from the statistics kernel, then the
   // module epilogue (grad_w + weight-LSQ backward, alpha_cim's quantiser, the step sizes) from there
@@ -763,11 +770,18 @@ int cimq_profile_start(int kernel_id, int max_launches) {
   if (kernel_id < KID_FWD || kernel_id > KID_LAST || max_launches <= 0)
     return fail(CIMQ_EINVAL, "bad profiler arguments");
   p.ev = new hipEvent_t[2 * (size_t)max_launches];
+  p.lb = new double[(size_t)max_launches];
+  p.lf = new double[(size_t)max_launches];
+  p.lm = new double[(size_t)max_launches];
   for (int i = 0; i < 2 * max_launches; ++i) {
     if (hipEventCreate(&p.ev[i]) != hipSuccess) {
       for (int k = 0; k < i; ++k) (void)hipEventDestroy(p.ev[k]);
       delete[] p.ev;
+      delete[] p.lb;
+      delete[] p.lf;
+      delete[] p.lm;
       p.ev = nullptr;
+      p.lb = p.lf = p.lm = nullptr;
       return fail(CIMQ_EHIP, "hipEventCreate");
     }
   }
@@ -775,6 +789,25 @@ int cimq_profile_start(int kernel_id, int max_launches) {
   p.cap = max_launches;
   p.n = 0;
   p.bytes = p.flops = 0;
+  return CIMQ_OK;
+}
+
+int cimq_profile_read(int cap, double* ms, double* algo_bytes, double* algo_flops, double* mfma_ops, int* launches) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (!p.ev) return fail(CIMQ_EINVAL, "profiler not running");
+  if (cap < 0 || (cap > 0 && (!ms || !algo_bytes || !algo_flops || !mfma_ops))) return fail(CIMQ_EINVAL, "bad buffers");
+  const int n = std::min(cap, p.n);
+  for (int i = 0; i < n; ++i) {
+    float t = 0;
+    if (hipEventSynchronize(p.ev[2 * i + 1]) != hipSuccess || hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]) != hipSuccess)
+      return fail(CIMQ_EHIP, "hipEventElapsedTime");
+    ms[i] = t;
+    algo_bytes[i] = p.lb[i];
+    algo_flops[i] = p.lf[i];
+    mfma_ops[i] = p.lm[i];
+  }
+  if (launches) *launches = p.n;
   return CIMQ_OK;
 }
 
@@ -799,7 +832,11 @@ int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, doubl
   if (algo_flops) *algo_flops = p.flops;
   for (int i = 0; i < 2 * p.cap; ++i) (void)hipEventDestroy(p.ev[i]);
   delete[] p.ev;
+  delete[] p.lb;
+  delete[] p.lf;
+  delete[] p.lm;
   p.ev = nullptr;
+  p.lb = p.lf = p.lm = nullptr;
   p.kid = KID_NONE;
   p.cap = p.n = 0;
   return rc;

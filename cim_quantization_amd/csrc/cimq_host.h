@@ -14,7 +14,7 @@
 #include <string>
 
 #include "../../include/cimq.h"
-#include "cimq_v7.hip"
+#include "cimq_fused.hip"
 
 
 namespace cimq {
@@ -451,6 +451,61 @@ inline Plan7 v7_plan(const Geo& g) {
   return p;
 }
 
+// ---- the fused backward (cimq_fused.hip): one kernel per stride-1 3x3 w2a2 / w3a3 layer ----
+struct Plan9 {
+  bool ok;
+  V9 v;
+};
+
+inline Plan9 v9_plan(const Geo& g) {
+  Plan9 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("FUSED", 1) == 0) return p;
+  const Plan7 p7 = v7_plan(g);
+  if (!p7.ok) return p;
+  if (g.NBP != 4 || g.nbw != g.nba || (g.nbw != 2 && g.nbw != 3)) return p;
+  if (g.SH != 1 || g.SW != 1 || g.KHW != 9) return p;
+  if (g.W < 8 || g.W > 64 || (g.W & (g.W - 1)) != 0 || g.Wo != g.W) return p;
+  if (g.O != g.Opad || g.O > 64) return p;
+  V9& v = p.v;
+  v.lw = 0;
+  while ((1 << v.lw) < g.W) ++v.lw;
+  v.R = 64 / g.W;
+  if (g.H % v.R != 0 || g.Ho != g.H) return p;
+  v.nsteps = g.H / v.R;
+  v.SWD = std::min(16, g.W);
+  v.NSEG = g.W / v.SWD;
+  v.RSLOT = v.nsteps == 1 ? g.H : v.R + 2;
+  v.NCPBT = p7.v.NCPBT;
+  v.lcin = p7.v.lcin;
+  v.NCG = 0;
+  for (int i = 0; i < g.T; ++i) {
+    const int c0 = (i * g.xbar) / 9, c1 = (std::min(g.K, (i + 1) * g.xbar) - 1) / 9;
+    v.NCG = std::max(v.NCG, c1 - c0 + 1);
+  }
+  if (v.NCG > 16) return p;
+  v.PROWS = v.R + 2;
+  v.CPITCH = v.PROWS * g.W + 8;
+  v.KWP = v.NCG * v.CPITCH;
+  v.nitems = v.NCG * v.PROWS * (g.W / 8);
+  if (v.nitems > 512) return p;
+  v.NGRP = (g.K + 15) / 16;
+  v.gwl = v.nsteps > 1 ? 1 : 0;
+  const int nkj = g.nbw * g.nba;
+  size_t o = 0;
+  v.o_ring = (unsigned)o; o += a16((size_t)v.RSLOT * v.NSEG * 3 * g.C * (v.SWD + 2) * 4);
+  v.o_cel = (unsigned)o; o += a16((size_t)2 * nkj * 4);
+  v.o_red = (unsigned)o; o += 64;
+  v.o_plane = (unsigned)o; o += a16((size_t)g.nba * 3 * v.KWP * 2);
+  v.o_gwl = (unsigned)o; o += v.gwl ? a16((size_t)v.NGRP * 16 * g.Opad * 4) : 0;
+  v.o_gal = (unsigned)o; o += a16((size_t)4 * g.T * nkj * 16 * 4);
+  v.o_st = (unsigned)o; o += a16((size_t)64 * g.O * 4);
+  v.o_g = (unsigned)o; o += a16((size_t)g.O * 68 * 4);
+  v.lds = (unsigned)o;
+  p.ok = o <= kLdsMax - 512;
+  return p;
+}
+
 // ---- the dense path (cimq_part_dense.hip): 1x1 kernels on 1x1 images, a [B][C] x [C][O] GEMM ----
 // (BASELINE cfg5, QuantLinear as Conv2dLSQCiM(k=1) on [B, C, 1, 1]); the library ternary ADC, equal
 // weight / activation slice counts up to 4 (the uint2 state word holds 16 slice pairs per plane)
@@ -502,8 +557,9 @@ inline WsLayout ws_layout(const Geo& g) {
   gw_chunks(g, &W.rows, &W.nchunks);
   // backward slabs: the v7 grad_w kernel's pixel chunks when it applies (the alpha_cim init
   // kernel keeps gw_chunks' split: W.nchunks / W.rows)
+  // (the fused backward: one chunk per image)
   const Plan7 p7 = v7_plan(g);
-  W.nchunks_bwd = p7.ok ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
+  W.nchunks_bwd = v9_plan(g).ok ? g.B : p7.ok ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
   const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
@@ -556,9 +612,10 @@ inline int set_lds(K kernel, size_t bytes) {
 // 1-4: every launch of that role (all kernel variants); 5-7: only the v7-path kernels
 // (cim_fwd_v3_kernel<4, KS, true>, cim_bwd_gx_v8_kernel, cim_bwd_gw_v7_kernel), so that one
 // id maps to the launches of one rocprof kernel symbol family
+// (8: the fused backward, cimq_fused.hip -- grad_x and grad_w in one launch, role grad_x)
 enum KernelId {
   KID_NONE = 0, KID_FWD = 1, KID_BWD_GX = 2, KID_BWD_GW = 3, KID_PREP_ACT = 4,
-  KID_FWD_V7 = 5, KID_GX_V8 = 6, KID_GW_V7 = 7, KID_LAST = 7
+  KID_FWD_V7 = 5, KID_GX_V8 = 6, KID_GW_V7 = 7, KID_FUSED = 8, KID_LAST = 8
 };
 
 struct Profiler {
@@ -567,24 +624,40 @@ struct Profiler {
   int cap = 0, n = 0;
   hipEvent_t* ev = nullptr;  // 2*cap
   double bytes = 0, flops = 0;
+  // per launch: algorithmic bytes, logical flops, MFMA operations as issued (cimq_profile_read)
+  double *lb = nullptr, *lf = nullptr, *lm = nullptr;
 };
 inline Profiler& prof() {
   static Profiler p;
   return p;
 }
 
-inline void algo_counts(const Geo& g, int kid, double* bytes, double* flops) {
+// slice pairs whose binary_mask entry is nonzero: 2^(bsa*j + bsw*k) wraps to 0 in int8 at >= 2^8
+// (_quan_base.py:207-214), so the w8a8 first layer has 36 live pairs of 64
+inline int live_pairs(const Geo& g) {
+  int n = 0;
+  for (int k = 0; k < g.nbw; ++k)
+    for (int j = 0; j < g.nba; ++j) n += (g.bsa * j + g.bsw * k <= 7) ? 1 : 0;
+  return n;
+}
+
+// SURVEY 8(d) per launch: *bytes = the fp32 tensors the kernel must read or write once, *flops = the
+// logical 2*MAC (times the slice count the contraction runs over), *mops = the MFMA operations as the
+// algorithm issues them: int8 bit-slice products of the live pairs (forward), three bf16 products per
+// fp32-accurate backward MAC
+inline void algo_counts(const Geo& g, int kid, double* bytes, double* flops, double* mops) {
   const double x4 = 4.0 * (double)g.Nin, y4 = 4.0 * (double)g.M * g.O;
   const double mac = (double)g.M * g.O * g.K;
   switch (kid) {
     case KID_FWD_V7:
-    case KID_FWD: *bytes = x4 + y4; *flops = 2.0 * mac; break;             // read x, write y
+    case KID_FWD: *bytes = x4 + y4; *flops = 2.0 * mac; *mops = 2.0 * mac * live_pairs(g); break;  // read x, write y
     case KID_GX_V8:
-    case KID_BWD_GX: *bytes = 2.0 * x4 + y4; *flops = 2.0 * mac * g.nbw; break;  // read gy, x; write gx
+    case KID_BWD_GX: *bytes = 2.0 * x4 + y4; *flops = 2.0 * mac * g.nbw; *mops = 3.0 * *flops; break;  // read gy, x; write gx
     case KID_GW_V7:
-    case KID_BWD_GW: *bytes = x4 + y4; *flops = 2.0 * mac * g.nba; break;  // read gy, x
-    case KID_PREP_ACT: *bytes = x4 + (double)g.Nin * (g.NBP + 1); *flops = 0; break;
-    default: *bytes = 0; *flops = 0;
+    case KID_BWD_GW: *bytes = x4 + y4; *flops = 2.0 * mac * g.nba; *mops = 3.0 * *flops; break;  // read gy, x
+    case KID_PREP_ACT: *bytes = x4 + (double)g.Nin * (g.NBP + 1); *flops = 0; *mops = 0; break;
+    case KID_FUSED: *bytes = 2.0 * x4 + y4; *flops = 2.0 * mac * (g.nbw + g.nba); *mops = 3.0 * *flops; break;  // read gy, x; write gx
+    default: *bytes = 0; *flops = 0; *mops = 0;
   }
 }
 
@@ -593,13 +666,17 @@ inline int prof_begin(int kid, const Geo& g, hipStream_t s) {
   Profiler& p = prof();
   std::lock_guard<std::mutex> lk(p.mu);
   if (p.n >= p.cap) return -1;
-  const int role = kid == KID_FWD_V7 ? KID_FWD : kid == KID_GX_V8 ? KID_BWD_GX : kid == KID_GW_V7 ? KID_BWD_GW : kid;
+  const int role = kid == KID_FWD_V7 ? KID_FWD : (kid == KID_GX_V8 || kid == KID_FUSED) ? KID_BWD_GX
+                 : kid == KID_GW_V7 ? KID_BWD_GW : kid;
   if (p.kid != kid && p.kid != role) return -1;
   const int slot = p.n++;
-  double b, f;
-  algo_counts(g, kid, &b, &f);
+  double b, f, mo;
+  algo_counts(g, kid, &b, &f, &mo);
   p.bytes += b;
   p.flops += f;
+  p.lb[slot] = b;
+  p.lf[slot] = f;
+  p.lm[slot] = mo;
   (void)hipEventRecord(p.ev[2 * slot], s);
   return slot;
 }
@@ -639,6 +716,9 @@ int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* s
   int launch_v7_n<NBW, NBA>(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa, \
                             const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, \
                             const Carry& carry)
+// cimq_part_fused.hip: the fused backward (v9_plan)
+int launch_fused(const Geo& g, const Plan9& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+                 const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry);
 extern template CIMQ_V7_SIG(2, 2);
 extern template CIMQ_V7_SIG(3, 3);
 extern template CIMQ_V7_SIG(8, 8);

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 8
+#define CIMQ_ABI_VERSION 9
 
 /* status codes */
 #define CIMQ_OK 0
@@ -330,12 +330,18 @@ int cimq_qconv_backward_scales(const cimq_qconv_desc* d, const float* grad_y, co
 
 /* Diagnostic kernel timer.  Until cimq_profile_stop(), every launch of kernel ``kernel_id``
  * (1 = partial-sum forward, 2 = grad_x, 3 = grad_w/grad_alpha, 4 = act-code prep, each over
- * all kernel variants; 5 / 6 / 7 = only the v7-path forward / grad_x / grad_w kernels) is
+ * all kernel variants; 5 / 6 / 7 = only the v7-path forward / grad_x / grad_w kernels; 8 = the
+ * fused backward of the stride-1 w2a2 / w3a3 layers, role 2) is
  * bracketed by a hipEvent pair on its launch stream (at most ``max_launches``).  stop()
  * waits for the last event and returns the summed kernel time, the number of launches and
  * their summed algorithmic bytes / flops ("Roofline accounting"). */
 int cimq_profile_start(int kernel_id, int max_launches);
 int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, double* algo_flops);
+/* ABI 9: before cimq_profile_stop(), the first ``cap`` launches one by one -- HIP-event duration (ms),
+ * the SURVEY 8(d) algorithmic bytes and logical flops, and the MFMA operations as issued (int8 bit-slice
+ * products of the live slice pairs forward, three bf16 products per fp32-accurate backward MAC) -- and
+ * in *launches the count recorded.  Lets a caller take max(t_HBM, t_MFMA) per launch. */
+int cimq_profile_read(int cap, double* ms, double* algo_bytes, double* algo_flops, double* mfma_ops, int* launches);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,9 @@
 
     rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir_f> -o p -- python bench.py ...
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir_w> -o p -- python bench.py ...
-    python tools/pmc_traffic.py <dir_f>/p_counter_collection.csv <dir_w>/p_counter_collection.csv > traffic.json
+    rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d <dir_v> -o p -- python bench.py ...   (optional)
+    python tools/pmc_traffic.py <dir_f>/p_counter_collection.csv <dir_w>/p_counter_collection.csv \
+        [<dir_v>/p_counter_collection.csv] > traffic.json
 
 Per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B / lane) streaming read, so
@@ -34,10 +36,13 @@ def per_kernel(path, counter):
 
 fetch, nf = per_kernel(sys.argv[1], "FETCH_SIZE")
 write, _ = per_kernel(sys.argv[2], "WRITE_SIZE")
+valu = per_kernel(sys.argv[3], "SQ_INSTS_VALU")[0] if len(sys.argv) > 3 else {}
+waves = per_kernel(sys.argv[3], "SQ_WAVES")[0] if len(sys.argv) > 3 else {}
 from bench import source_sha  # noqa: E402
 
 out = {"_meta": {"source_sha": source_sha()}}
 for k in sorted(set(fetch) | set(write)):
     out[k] = {"fetch_kib": fetch.get(k), "write_kib": write.get(k), "dispatches": nf.get(k, 0),
-              "traffic_bytes": (2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024.0}
+              "traffic_bytes": (2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024.0,
+              "valu_insts": valu.get(k), "waves": waves.get(k)}
 json.dump(out, sys.stdout, indent=1)
