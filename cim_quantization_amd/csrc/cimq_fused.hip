@@ -59,7 +59,11 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
   constexpr int NKJ = NB * NB;
   constexpr int NKS = (NB * OBX + 1) / 2;
   constexpr int WPO = 4 / OBX;  // grad_w waves per 16-channel output block
-  constexpr int NGW = 8 / WPO;  // 16-row groups per grad_w wave and tile (xbar <= 128)
+  // one output block (O = 16): its four waves split the two K-steps x two row-group halves, and each
+  // K-step half keeps its own grad_w accumulator in LDS; else the waves of a block split the row groups
+  constexpr int KSP = OBX == 1 ? 2 : 1;
+  constexpr int RGS = WPO / KSP;  // row-group stride of one wave
+  constexpr int NGW = 8 / RGS;    // 16-row groups per grad_w wave and tile (xbar <= 128)
   constexpr int O = 16 * OBX;   // v9_plan: O is a multiple of 16
   constexpr int PST = (16 * O + 511) / 512;  // 16-B pieces of a unit's state words / grad_out per thread
   constexpr int GP = 68;        // grad_out LDS row pitch (floats): 16-B reads of 16 channels hit distinct banks
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
   }
   if (threadIdx.x < NB) *reinterpret_cast<uint4*>(pl + (size_t)threadIdx.x * 3 * v.KWP + zoff) = make_uint4(0u, 0u, 0u, 0u);
   if (v.gwl)
-    for (int t = threadIdx.x; t < v.NGRP * 16 * O; t += blockDim.x) gwl[t] = 0.f;
+    for (int t = threadIdx.x; t < KSP * v.NGRP * 16 * O; t += blockDim.x) gwl[t] = 0.f;
   for (int t = threadIdx.x; t < 4 * g.T * NKJ * 16; t += blockDim.x) gal[t] = 0.f;
   __syncthreads();
   // standard binary masks (_quan_base.py:207-214): cE_kj = 2^(bsw*k), cD_kj = 2^(bsa*j) for every pair;
@@ -120,7 +124,10 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
   const int seg = gq_ow >> lsw, col = gq_ow & (v.SWD - 1);
   // grad_w: output block and share of the row groups
   const int gwi = wave - 4;
-  const int gob = gxw ? 0 : gwi / WPO, wpart = gxw ? 0 : gwi % WPO;
+  const int gob = gxw ? 0 : gwi / WPO, within = gxw ? 0 : gwi % WPO;
+  const int ksel = KSP == 2 ? (within & 1) : 0;                  // KSP 2: this wave's K-step
+  const int wpart = KSP == 2 ? (within >> 1) : within;            // its row groups: wpart + RGS * n
+  float* gwk = gwl + (size_t)(KSP == 2 ? ksel : 0) * v.NGRP * 16 * O;  // its grad_w accumulator
   const int go = gob * 16 + r16;  // this lane's output channel (B column)
 
   // ---- the unit's global loads, issued one unit ahead into registers, staged into LDS at its start ----
@@ -307,11 +314,11 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       const int flo = i * g.xbar;
       const int ngt = (min(g.xbar, g.K - flo) + 15) >> 4;  // row groups of tile i
       const int c0 = flo / 9;
-      // this wave's row groups gr = wpart + WPO * n; per lane the plane offset of its row (or -1)
+      // this wave's row groups gr = wpart + RGS * n; per lane the plane offset of its row (or -1)
       int gofs[NGW];
 #pragma unroll
       for (int n = 0; n < NGW; ++n) {
-        const int gr = wpart + WPO * n;
+        const int gr = wpart + RGS * n;
         const int f = flo + 16 * gr + r16;
         gofs[n] = -1;
         if (gr < ngt && f < min(g.K, flo + g.xbar)) {
@@ -324,6 +331,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       for (int n = 0; n < NGW; ++n) acc[n] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
+        if (KSP == 2 && ks != ksel) continue;  // uniform: the other K-step's waves
         const int q0 = 32 * ks + 8 * g4;  // first pixel of this lane's 8 (one row segment)
         uint32_t sv[8];
         float gv[8];
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           gv[0] = a0.x; gv[1] = a0.y; gv[2] = a0.z; gv[3] = a0.w;
           gv[4] = a1.x; gv[5] = a1.y; gv[6] = a1.z; gv[7] = a1.w;
         }
-        if (WPO == 1 || wpart == ks) {
+        if (KSP == 2 ? wpart == 0 : (WPO == 1 || wpart == ks)) {  // one wave per (block, K-step)
           // grad_alpha partials (lsq.py:321-333): the code is the signed 2-bit field {nz, neg}
 #pragma unroll
           for (int kj = 0; kj < NKJ; ++kj) {
@@ -370,7 +378,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
         }
 #pragma unroll
         for (int n = 0; n < NGW; ++n) {
-          if (wpart + WPO * n >= ngt) continue;  // uniform
+          if (wpart + RGS * n >= ngt) continue;  // uniform
           const int ofs = gofs[n] >= 0 ? gofs[n] + q0 : zoff;
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
@@ -385,13 +393,13 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       // accumulator rows 16 gr + 4 g4 + r, column o: owned by this wave alone
 #pragma unroll
       for (int n = 0; n < NGW; ++n) {
-        const int gr = wpart + WPO * n;
+        const int gr = wpart + RGS * n;
         if (gr >= ngt) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int fl = 16 * gr + 4 * g4 + r;
           if (v.gwl) {
-            gwl[(size_t)(flo + fl) * O + go] += acc[n][r];
+            gwk[(size_t)(flo + fl) * O + go] += acc[n][r];
           } else {
             gw_slab[(((size_t)b * g.T + i) * (g.FBT * 16) + fl) * O + go] = acc[n][r];
           }
@@ -461,7 +469,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
     for (int t = threadIdx.x; t < g.K * O; t += blockDim.x) {
       const int f = t / O, o = t - f * O;
       const int i = f / g.xbar, fl = f - i * g.xbar;
-      gw_slab[(((size_t)b * g.T + i) * FR + fl) * O + o] = gwl[t];
+      gw_slab[(((size_t)b * g.T + i) * FR + fl) * O + o] = KSP == 2 ? gwl[t] + gwl[(size_t)v.NGRP * 16 * O + t] : gwl[t];
     }
   }
   // grad_alpha: the waves of an output block that summed K-steps 0 / 1, in that order

@@ -981,22 +981,23 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   sm.rowinfo = reinterpret_cast<int4*>(smem + off); off += sizeof(int4) * 64;
   const int tlen = g.KS * 64;
   const int nkj = g.nbw * g.nba;
-  const int ncol = 32;
-  // [4 waves][nkj][32]: sums of code*g (INIT: of |u|), one writer lane per slot and wave, the
+  constexpr int NOBG = 1;  // 16-channel output blocks per workgroup (LDS: the per-wave sums below)
+  const int ncol = 16 * NOBG;
+  // [4 waves][nkj][ncol]: sums of code*g (INIT: of |u|), one writer lane per slot and wave, the
   // waves added in a fixed order at the end -- no atomics, bit-identical run to run
   float* qacc = reinterpret_cast<float*>(smem + off);
   off += sizeof(float) * 4 * nkj * ncol;
-  float* gwacc = reinterpret_cast<float*>(smem + off);  // [FBT*16][32]
-  off += sizeof(float) * g.FBT * 16 * ncol;
-  float* qbacc = reinterpret_cast<float*>(smem + off);  // [4 waves][nkj][32]: sum beta_term*g (shift variants)
-  off += sizeof(float) * 4 * nkj * ncol;
+  // [FBT*16][ncol] block sum of grad_w: built after the pixel loop, in the act-tile region (free by then)
+  float* gwacc = reinterpret_cast<float*>(smem);
+  float* qbacc = reinterpret_cast<float*>(smem + off);  // [4 waves][nkj][ncol]: sum beta_term*g (shift variants only)
+  off += is_shift(g) ? sizeof(float) * 4 * nkj * ncol : 0;
   int8_t* Xb = reinterpret_cast<int8_t*>(smem + off);   // [nba][tlen][64] bwd slices, f-major
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int i = blockIdx.y;
-  const int og = blockIdx.z;  // 32-channel group: o-blocks 2*og, 2*og+1
-  const int nob = min(2, g.OB16 - og * 2);
+  const int og = blockIdx.z;  // channel group: o-blocks NOBG*og ..
+  const int nob = min(NOBG, g.OB16 - og * NOBG);
   const int mc = blockIdx.x;
   const int mbeg = mc * rows_per_chunk, mend = min(mbeg + rows_per_chunk, g.M);
   const float sw = *sw_p, sa = *sa_p;
@@ -1006,10 +1007,8 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const bool shift = is_shift(g);
 
   for (int t = threadIdx.x; t < 4 * nkj * ncol; t += blockDim.x) qacc[t] = 0.f;
-  if (!INIT)
+  if (!INIT && shift)
     for (int t = threadIdx.x; t < 4 * nkj * ncol; t += blockDim.x) qbacc[t] = 0.f;
-  if (!INIT)
-    for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
   v4f gwa[FBMAX][2];
 #pragma unroll
   for (int a = 0; a < FBMAX; ++a) { gwa[a][0] = v4f{0, 0, 0, 0}; gwa[a][1] = v4f{0, 0, 0, 0}; }
@@ -1050,7 +1049,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
     for (int ob = 0; ob < 2; ++ob) {
       if (ob < nob) {
         const int ocol = ob * 16 + r16;
-        const int o = og * 32 + ocol;
+        const int o = og * ncol + ocol;
         float gval[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1070,7 +1069,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
             for (int ks = 0; ks < 4; ++ks)
               if (ks < g.KS) xa[ks] = load_xfrag(g, sm.As, j, wave * 16 + r16, ks, lane);
             for (int k = 0; k < g.nbw; ++k) {
-              const int nb = k * g.OB16 + og * 2 + ob;
+              const int nb = k * g.OB16 + og * NOBG + ob;
               v4i acc = {0, 0, 0, 0};
 #pragma unroll
               for (int ks = 0; ks < 4; ++ks)
@@ -1179,6 +1178,8 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
 
   // ---- block reductions -> slabs (deterministic: the waves in a fixed order, no atomics) ----
   if (!INIT) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) gwacc[t] = 0.f;
     for (int w = 0; w < 4; ++w) {
       __syncthreads();
       if (wave == w) {
@@ -1197,7 +1198,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   const int wq = nkj * ncol;
   for (int t = threadIdx.x; t < nkj * ncol; t += blockDim.x) {
     const int q = t / ncol, col = t - q * ncol;
-    const int o = og * 32 + col;
+    const int o = og * ncol + col;
     if (o < g.Opad) {
       const int k = q / g.nba, j = q - k * g.nba;
       const float qv = ((qacc[t] + qacc[wq + t]) + qacc[2 * wq + t]) + qacc[3 * wq + t];
@@ -1210,7 +1211,7 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
   if (INIT) return;
   for (int t = threadIdx.x; t < g.FBT * 16 * ncol; t += blockDim.x) {
     const int fl = t / ncol, col = t - fl * ncol;
-    const int o = og * 32 + col;
+    const int o = og * ncol + col;
     if (o < g.Opad) gw_slab[(((size_t)mc * g.T + i) * (g.FBT * 16) + fl) * g.Opad + o] = gwacc[t];
   }
 }

@@ -14,7 +14,7 @@ int launch_gw(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
-  dim3 grid(W.nchunks, g.T, (g.OB16 + 1) / 2);
+  dim3 grid(W.nchunks, g.T, g.OB16);  // one 16-channel output block per workgroup
   const int slot = INIT ? -1 : prof_begin(KID_BWD_GW, g, s);
   const size_t lds = lds_gw(g);
   auto kern = cim_bwd_gw_kernel<NBP, FBMAX, INIT>;

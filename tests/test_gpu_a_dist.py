@@ -3,11 +3,11 @@ two processes share the one GPU, torch.distributed on gloo over device tensors.
 
 * bench.Trainer's real step -- prepare_weights, the chained module epilogues, GradBucket.own,
   broadcast_from and FlatSGD -- on three ResNet-20 layer shapes (the w8a8 first conv, a 16-channel
-  32x32 and a 64-channel 8x8 layer): each rank's local bucket matches the CPU module oracle run on
-  the same state and data (normwise 1e-5 per parameter, 1e-4 for the two scalar step sizes), the
-  exchanged bucket is the mean of the two ranks' buckets and of the two ranks' oracle gradients
-  (1e-5 of the mean of |terms|), and after three steps every parameter is bit-identical across
-  the ranks;
+  32x32 and a 64-channel 8x8 layer) at batch 64 per rank: each rank's local bucket matches the CPU
+  module oracle run on the same state and data (normwise 1e-5 per tensor parameter; the two scalar
+  step sizes within 1e-5 of their sum of |terms|), the exchanged bucket is the mean of the two
+  ranks' buckets and of the two ranks' oracle gradients (1e-5 of the mean of |terms|), and after
+  three steps every parameter is bit-identical across the ranks;
 * bench.py's own world > 1 branch, launched by torch.distributed.run with the gloo backend.
 
 The ranks are child processes; this (parent) process never touches the GPU -- no HIP call, not even
@@ -36,7 +36,7 @@ def gpu_present():
         pytest.skip("no ROCm device")
 
 LAYERS = [("conv1", 3, 16, 32, 1, 8), ("layer1.0.conv1", 16, 16, 32, 1, 3), ("layer3.1.conv1", 64, 64, 8, 1, 3)]
-BATCH = 4
+BATCH = 64
 
 
 def _free_port():
@@ -47,17 +47,39 @@ def _free_port():
     return port
 
 
+def _lsq_terms(v, g_q, s, qn, qp, gscale):
+    """sum of |terms| of d loss / d alpha through the LSQ quantiser (lsq.py:547-555)."""
+    import numpy as np
+    v, g_q = v.astype(np.float64), g_q.astype(np.float64)
+    y = v / float(s)
+    r = np.rint(np.clip(y, qn, qp))
+    inside = (y >= qn) & (y <= qp)
+    return gscale * (np.abs(g_q * r).sum() + np.abs(np.where(inside, g_q * float(s), 0) * y / float(s)).sum())
+
+
 def _oracle_grads(layers, xs, gs):
-    """Local gradients of the CPU module oracle from each layer's current state, by parameter name."""
+    """Local gradients of the CPU module oracle from each layer's current state, by parameter name, and
+    the sums of |terms| of the two step-size gradients."""
+    import math
+
     from oracle import cim_module_oracle as cmo
     res = []
     for (name, c, o, h, s, nb), m, x, g in zip(LAYERS, layers, xs, gs):
         om = cmo.OracleConv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
                                     abitslice=1, xbar=128, adcbits=1.5)
+        om.debug_retain = True
         om.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=False)
         om.train()
-        om(x.detach().cpu()).backward(g.detach().cpu())
-        res.append({n: p.grad.detach().clone() for n, p in om.named_parameters()})
+        xc = x.detach().cpu()
+        om(xc).backward(g.detach().cpu())
+        d = om.dbg
+        (qn_a, qp_a), (qn_w, qp_w) = d["qa"], d["qw"]
+        w = om.weight.detach().numpy()
+        terms = {"alpha_act": _lsq_terms(xc.numpy(), d["x_q"].grad.numpy(), d["sa"].item(), qn_a, qp_a,
+                                         1.0 / math.sqrt(xc.numel() * qp_a)),
+                 "alpha_weight": _lsq_terms(w, d["w_q"].grad.numpy(), d["sw"].item(), qn_w, qp_w,
+                                            1.0 / math.sqrt(w.size * qp_w))}
+        res.append(({n: p.grad.detach().clone() for n, p in om.named_parameters()}, terms))
     return res
 
 
@@ -80,12 +102,18 @@ def _trainer_worker(rank, world, port, out):
         tr.compute(xs, gs)
         torch.cuda.synchronize()
         errs = []
-        for m, r in zip(layers, ref):
+        for m, (r, tt) in zip(layers, ref):
             for n, p in m.named_parameters():
                 d = (p.grad.detach().cpu() - r[n]).abs().max().item()
-                # normwise 1e-5; the two scalar step sizes (sums over the whole batch) within 1e-4
-                errs.append((n, d / (r[n].abs().max().item() + 1e-30) / (10.0 if p.numel() == 1 else 1.0)))
-        ref_flat = torch.cat([r[n].reshape(-1) for m, r in zip(layers, ref) for n, _ in m.named_parameters()])
+                # normwise 1e-5; the two scalar step sizes (sums over the whole batch): 1e-5 of their terms
+                errs.append((n, d / (tt[n] if p.numel() == 1 else r[n].abs().max().item() + 1e-30)))
+        ref_flat = torch.cat([r[n].reshape(-1) for m, (r, _) in zip(layers, ref) for n, _ in m.named_parameters()])
+        # per parameter of the flat bucket: the scalar's sum of |terms| (else 0), for the exchanged check
+        t_flat = torch.cat([torch.full((p.numel(),), float(tt[n]) if p.numel() == 1 else 0.0, dtype=torch.float64)
+                            for m, (_, tt) in zip(layers, ref) for n, p in m.named_parameters()])
+        t_all = [torch.zeros_like(t_flat) for _ in range(world)]
+        dist.all_gather(t_all, t_flat)
+        t_mean = sum(t_all) / world
         gathered = [torch.zeros_like(ref_flat) for _ in range(world)]
         dist.all_gather(gathered, ref_flat)
         mean_ref = sum(gathered) / world
@@ -103,8 +131,8 @@ def _trainer_worker(rank, world, port, out):
             for _, p in m.named_parameters():
                 k = p.numel()
                 seg, rs, ra = exch[off:off + k], mean_ref[off:off + k], abs_ref[off:off + k]
-                e = (seg - rs).abs().max().item() / (ra.max().item() + 1e-30)
-                exch_err = max(exch_err, e / (10.0 if k == 1 else 1.0))
+                scale = float(t_mean[off]) if k == 1 else ra.max().item() + 1e-30
+                exch_err = max(exch_err, (seg - rs).abs().max().item() / scale)
                 off += k
         tr.opt.step()
         tr.flat.zero_()
