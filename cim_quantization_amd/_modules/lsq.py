@@ -94,8 +94,10 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         return super()._load_from_state_dict(*args, **kwargs)
 
     def _init_flags(self):
-        if self._state_cache is None:
+        key = (self.init_state._version, self.init_state_cim._version)
+        if self._state_cache is None or getattr(self, "_state_key", None) != key:
             self._state_cache = [bool(self.init_state.item() != 0), bool(self.init_state_cim.item() != 0)]
+            self._state_key = key
         return self._state_cache
 
     def forward(self, x):
@@ -175,20 +177,25 @@ class _HostFlags:
 
     The reference tests ``self.init_state == 0`` (and ActLSQ ``self.signed == 1``) on every
     forward (lsq.py:407, :601, :628, :634, :643); on a GPU tensor each test is a device sync that stalls the
-    launch queue. The values are read once and cached. The cache is reset by load_state_dict
-    and by dist.GradBucket.broadcast_from; code that writes the buffers directly sets
-    ``_state_cache = None``, as for Conv2dLSQCiM."""
+    launch queue. The values are read once and cached, keyed by the buffers' version counters: any
+    in-place write to them -- load_state_dict, dist.GradBucket.broadcast_from, torch DDP's buffer
+    broadcast from rank 0 before every forward (train.py:232 wraps the model in DDP) -- bumps the counter
+    and the next forward re-reads them, so a rank follows rank 0's buffers as the reference does.  Writes
+    through ``.data`` (which bypass the counter) update the cache alongside."""
 
     _state_cache = None
+    _state_key = None
 
     def _load_from_state_dict(self, *args, **kwargs):
         self._state_cache = None
         return super()._load_from_state_dict(*args, **kwargs)
 
     def _flags(self):
-        if self._state_cache is None:
-            sg = getattr(self, "signed", None)
+        sg = getattr(self, "signed", None)
+        key = (self.init_state._version, -1 if sg is None else sg._version)
+        if self._state_cache is None or self._state_key != key:
             self._state_cache = [bool(self.init_state.item() != 0), sg is not None and bool(sg.item() == 1)]
+            self._state_key = key
         return self._state_cache
 
 

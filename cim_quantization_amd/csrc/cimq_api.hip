@@ -69,6 +69,20 @@ static Carry no_carry() {
 int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                      const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused,
                      const Carry& carry = no_carry()) {
+  if (!v7_bwd(g)) {
+    if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
+    if (dense_plan(g)) {
+      *lsq_fused = false;
+      return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s);
+    }
+    return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
+  }
+  const PlanC1 pc = c1_plan(g);
+  if (pc.ok) {
+    const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
+    *lsq_fused = lsq;
+    return launch_c1(g, pc, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+  }
   const Plan9 p9 = v9_plan(g);
   if (p9.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
@@ -115,9 +129,10 @@ int launch_reduce_slab(const Geo& g, const uint8_t* ctx, uint8_t* ws, size_t sla
 // number of act-LSQ partials the backward leaves in ws (fused into the fused / v7 grad_x kernels,
 // else one per lsq_act_bwd_kernel block)
 int act_parts(const Geo& g) {
-  if (v9_plan(g).ok) return g.B;
-  const Plan7 p7 = v7_plan(g);
-  if (p7.ok) return g.B * p7.v.nbands;
+  if (v7_bwd(g)) {
+    if (v9_plan(g).ok || c1_plan(g).ok) return g.B;
+    return g.B * v7_plan(g).v.nbands;
+  }
   int grid = cdiv(g.Nin, 256);
   return grid > kLsqParts ? kLsqParts : grid;
 }
@@ -259,7 +274,8 @@ int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* cod
   Geo g;
   CIMQ_TRY(make_geo(d, &g));
   if (!ctx || !code_out || !pass_out) return fail(CIMQ_EINVAL, "null pointer argument");
-  if (!v7_plan(g).ok) return fail(CIMQ_EUNSUPPORTED, "this layer's forward writes no v7 state words");
+  if (!v7_plan(g).ok || c1_plan(g).ok)
+    return fail(CIMQ_EUNSUPPORTED, "this layer's forward writes no v7 state words (the first conv's backward recomputes them)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
   const long long n = (long long)g.T * g.M * g.O;

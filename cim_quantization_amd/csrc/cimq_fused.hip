@@ -203,6 +203,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
         if (i == 0) *reinterpret_cast<float4*>(gl + (t >> 4) * GP + (t & 15) * 4) = gvc[q];
       }
     }
+#ifndef CIMQ_EXP_F_NOSTAGE  // attribution builds only (tools/kernel_experiment.py): skip a part of the kernel
     if (it < v.nitems) {
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
         }
       }
     }
+#endif
     // the next unit's loads go out now, behind this unit's work
     if (u + 1 < nunits) {
       const int s_n = (u + 1) / g.T, i_n = (u + 1) - s_n * g.T;
@@ -230,6 +232,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
     __syncthreads();  // the unit is in LDS
 
     if (gxw) {
+#ifndef CIMQ_EXP_F_NOGX
       // ================= grad_x: G from the state words, MFMA against wcy, ring =================
       v8bf Gh[NKS], Gm[NKS], Gl[NKS];
       uint4 sq[OBX];
@@ -309,7 +312,9 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           }
         }
       }
+#endif
     } else {
+#ifndef CIMQ_EXP_F_NOGW
       // ================= grad_w (+ grad_alpha): B = g * D_j, A from the planes =================
       const int flo = i * g.xbar;
       const int ngt = (min(g.xbar, g.K - flo) + 15) >> 4;  // row groups of tile i
@@ -405,6 +410,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           }
         }
       }
+#endif
     }
 
     if (i == g.T - 1) {

@@ -14,7 +14,7 @@
 #include <string>
 
 #include "../../include/cimq.h"
-#include "cimq_fused.hip"
+#include "cimq_c1.hip"
 
 
 namespace cimq {
@@ -527,7 +527,10 @@ inline Plan9 v9_plan(const Geo& g) {
   if (g.NBP != 4 || g.nbw != g.nba || (g.nbw != 2 && g.nbw != 3)) return p;
   if (g.SH != 1 || g.SW != 1 || g.KHW != 9) return p;
   if (g.W < 8 || g.W > 64 || (g.W & (g.W - 1)) != 0 || g.Wo != g.W) return p;
-  if (g.O != g.Opad || g.O > 64) return p;
+  // four 16-channel blocks only: on ResNet-20's layers the fused kernel measured 200 / 110 / 77 us per
+  // launch at 16 / 32 / 64 channels against 107 / 95 / 85 us for the v8 grad_x + v7 grad_w pair
+  // (DESIGN.md section 4): below four blocks a step has too little MFMA work to hide its staging
+  if (g.O != g.Opad || g.O != 64) return p;
   V9& v = p.v;
   v.lw = 0;
   while ((1 << v.lw) < g.W) ++v.lw;
@@ -567,6 +570,55 @@ inline Plan9 v9_plan(const Geo& g) {
   return p;
 }
 
+// ---- the first conv's backward from recomputed partial sums (cimq_c1.hip) ----
+struct PlanC1 {
+  bool ok;
+  VC1 v;
+};
+
+inline PlanC1 c1_plan(const Geo& g) {
+  PlanC1 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("C1", 1) == 0) return p;
+  const Plan7 p7 = v7_plan(g);
+  if (!p7.ok || g.variant != VAR_LIBRARY) return p;
+  if (g.NBP != 8 || g.nbw != 8 || g.nba != 8 || g.bsw != 1 || g.bsa != 1 || g.O != 16 || g.K > 32) return p;
+  if (g.SH != 1 || g.SW != 1 || g.KHW != 9 || g.T != 1) return p;
+  if (g.W < 8 || g.W > 64 || (g.W & (g.W - 1)) != 0 || g.Wo != g.W || g.Ho != g.H) return p;
+  VC1& v = p.v;
+  v.lw = 0;
+  while ((1 << v.lw) < g.W) ++v.lw;
+  v.R = 128 / g.W;
+  if (g.H % v.R != 0) return p;
+  v.nsteps = g.H / v.R;
+  v.RH = (v.R - 1) + 3;
+  v.WP = g.W + 2;
+  v.SWD = std::min(16, g.W);
+  v.NSEG = g.W / v.SWD;
+  v.RSLOT = v.nsteps == 1 ? g.H : v.R + 2;
+  v.NCPBT = p7.v.NCPBT;
+  v.lcin = p7.v.lcin;
+  size_t o = 0;
+  const size_t patch = a16((size_t)g.C * v.RH * v.WP * 8);
+  v.o_xp = (unsigned)o; o += patch;
+  v.o_hp = (unsigned)o; o += patch;
+  v.o_ptab = (unsigned)o; o += 64 * 4;
+  v.o_prm = (unsigned)o; o += 64 * 16 * 16;
+  v.o_cel = (unsigned)o; o += a16(3 * 64 * 4);
+  v.o_g = (unsigned)o; o += 16 * 132 * 4;
+  v.o_ring = (unsigned)o; o += a16((size_t)v.RSLOT * v.NSEG * 3 * g.C * (v.SWD + 2) * 4);
+  v.o_gal = (unsigned)o; o += 8 * 64 * 16 * 4;
+  v.o_red = (unsigned)o; o += a16((2 * 16 * 16 + 8) * 4);
+  v.o_e = (unsigned)o; o += 8 * 2 * 256 * 4;
+  v.o_wk = (unsigned)o; o += 8 * 64 * 16;
+  v.o_wc = (unsigned)o; o += (size_t)3 * 4 * 64 * 16;
+  v.lds = (unsigned)o;
+  // the kernel's one-step-ahead staging: at most three 16-byte items per thread of 512
+  if (2 * g.C * v.RH * (g.W / 2) + 512 > 3 * 512 || (g.K - 1) / 3 / 4 + 1 > 3) return p;
+  p.ok = o <= kLdsMax - 512;
+  return p;
+}
+
 // ---- the dense path (cimq_part_dense.hip): 1x1 kernels on 1x1 images, a [B][C] x [C][O] GEMM ----
 // (BASELINE cfg5, QuantLinear as Conv2dLSQCiM(k=1) on [B, C, 1, 1]); the library ternary ADC, equal
 // weight / activation slice counts up to 4 (the uint2 state word holds 16 slice pairs per plane)
@@ -602,6 +654,12 @@ inline bool shift_table_fits(const Geo& g) {
   return (size_t)g.nbw * g.nba * 16 * (2 * shift_table_range(g) + 1) * 4 <= 48 * 1024;
 }
 
+// the backward runs on the v7 plan's state words (v7 / fused / first-conv kernels): the library ADC, or
+// the shift ADC where the statistics kernel takes it; every other layer runs the general kernels
+inline bool v7_bwd(const Geo& g) {
+  return v7_plan(g).ok && (g.variant == VAR_LIBRARY || shift_stats_ok(g));
+}
+
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
   int rows, nchunks, nchunks_bwd;
@@ -618,9 +676,11 @@ inline WsLayout ws_layout(const Geo& g) {
   gw_chunks(g, &W.rows, &W.nchunks);
   // backward slabs: the v7 grad_w kernel's pixel chunks when it applies (the alpha_cim init
   // kernel keeps gw_chunks' split: W.nchunks / W.rows)
-  // (the fused backward: one chunk per image)
+  // (the one-kernel backwards: one chunk per image; the v7 plan also covers shift-ADC layers that the
+  // statistics kernel does not take -- those run the general backward)
   const Plan7 p7 = v7_plan(g);
-  W.nchunks_bwd = v9_plan(g).ok ? g.B : p7.ok ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
+  const bool v7b = v7_bwd(g);
+  W.nchunks_bwd = (v9_plan(g).ok || c1_plan(g).ok) ? g.B : v7b ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
   const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
@@ -643,7 +703,7 @@ inline WsLayout ws_layout(const Geo& g) {
   W.wpart = o; o = align256(o + sizeof(float) * 2 * (size_t)cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64));
   W.bpo = o; o = align256(o + sizeof(float) * (size_t)g.M * g.O);
   // the general backward's unfolded grad_x [M][K] (folded by fold_gx_kernel)
-  W.gxu = o; o = align256(o + ((p7.ok || dense_plan(g)) ? 0 : sizeof(float) * (size_t)g.M * g.K));
+  W.gxu = o; o = align256(o + ((v7b || dense_plan(g)) ? 0 : sizeof(float) * (size_t)g.M * g.K));
   W.total = o;
   return W;
 }
@@ -780,6 +840,8 @@ int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* s
 // cimq_part_fused.hip: the fused backward (v9_plan)
 int launch_fused(const Geo& g, const Plan9& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
                  const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry);
+int launch_c1(const Geo& g, const PlanC1& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+              const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry);
 extern template CIMQ_V7_SIG(2, 2);
 extern template CIMQ_V7_SIG(3, 3);
 extern template CIMQ_V7_SIG(8, 8);

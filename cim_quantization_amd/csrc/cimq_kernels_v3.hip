@@ -259,13 +259,17 @@ __device__ inline float adc3(float cf, uint64_t mhi, uint64_t mlo) {
 // CST: compact state words (cimq_v7.hip) -- one uint32 per (tile i, pixel m, channel o) at
 // st32[(i*M + m)*O + o], bits 3*(k*nba + j) + {0: STE pass, 1: code != 0, 2: code < 0}.
 // CST > 0 also fixes nbw = nba = CST at compile time: the ternary-threshold path then runs
+// (CSTA = 9: CST 8 without writing the state words -- the first conv's backward recomputes them)
 // fully unrolled (every slice pair's MFMAs issued before its ADC work, state bits shifted in).
-template <int NBP, int KS, int CST, int OBM>
+template <int NBP, int KS, int CSTA, int OBM>
 __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
                                                          const float* __restrict__ sa_p, float* __restrict__ out,
                                                          uint8_t* __restrict__ st) {
+  // CSTA 9: the w8a8 fast path of CST 8 without the state words (cimq_c1.hip recomputes them)
+  constexpr int CST = CSTA == 9 ? 8 : CSTA;
+  constexpr bool WST = CSTA != 9;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int og = blockIdx.y;
   const int NOB = min(OBM, g.OB16);
@@ -547,7 +551,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
           }
         }
       }
-      if (CST) {
+      if (CST && WST) {
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
           const int o = (og * OBM + ob) * 16 + r16;

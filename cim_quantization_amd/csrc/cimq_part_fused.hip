@@ -1,5 +1,6 @@
-// cimq_part_fused.hip -- launch of the fused backward (cimq_fused.hip) for the stride-1 3x3 w2a2 /
-// w3a3 layers v9_plan accepts: one workgroup per image, grad_x + grad_w + grad_alpha partials.
+// cimq_part_fused.hip -- launch of the one-kernel backwards: cimq_fused.hip for the stride-1 3x3 w2a2 /
+// w3a3 layers v9_plan accepts, cimq_c1.hip for the w8a8 first conv (c1_plan); one workgroup per image,
+// grad_x + grad_w + grad_alpha partials.
 // Own translation unit of libcimq.so.
 #include "cimq_host.h"
 
@@ -37,6 +38,22 @@ int launch_fused(const Geo& g, const Plan9& p, const uint8_t* ctx, const float* 
                  const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry) {
   if (g.nbw == 2) return launch_fused_n<2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
   return launch_fused_n<3>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+}
+
+int launch_c1(const Geo& g, const PlanC1& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+              const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry) {
+  CtxLayout L = ctx_layout(g);
+  WsLayout W = ws_layout(g);
+  Params pp = params_of(g, const_cast<uint8_t*>(ctx));
+  auto kern = lsq ? cim_bwd_c1_kernel<true> : cim_bwd_c1_kernel<false>;
+  CIMQ_TRY(set_lds(kern, p.v.lds));
+  const int slot = prof_begin(KID_FUSED, g, s);
+  hipLaunchKernelGGL(kern, dim3(g.B + (carry.finish ? 1 : 0)), dim3(512), p.v.lds, s, g, p.v, ctx + L.xcode, ctx + L.xhat,
+                     reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wfrag), reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wcy),
+                     pp, sw, sa, gout, x, gx, reinterpret_cast<float*>(ws + W.gw_slab),
+                     reinterpret_cast<float*>(ws + W.ga_slab), reinterpret_cast<float*>(ws + W.lsq_part), carry);
+  prof_end(slot, s);
+  return check_hip("cim_bwd_c1");
 }
 
 }  // namespace cimq

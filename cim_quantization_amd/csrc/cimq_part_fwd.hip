@@ -18,7 +18,8 @@ int launch_fwd_v3(const Geo& g, const Plan3& p, uint8_t* ctx, const float* sw, c
     kern = obm == 1 ? cim_fwd_v3_kernel<NBP, KS, 0, 1> : obm == 2 ? cim_fwd_v3_kernel<NBP, KS, 0, 2>
                                                        : cim_fwd_v3_kernel<NBP, KS, 0, 4>;
   } else if constexpr (NBP == 8) {
-    kern = cim_fwd_v3_kernel<8, KS, 8, 1>;  // v7_plan: w8a8 with one 16-channel block
+    // v7_plan: w8a8 with one 16-channel block; the first conv's backward (c1_plan) recomputes the state
+    kern = c1_plan(g).ok ? cim_fwd_v3_kernel<8, KS, 9, 1> : cim_fwd_v3_kernel<8, KS, 8, 1>;
   } else if (g.nbw == 2) {
     kern = obm == 1 ? cim_fwd_v3_kernel<NBP, KS, 2, 1> : obm == 2 ? cim_fwd_v3_kernel<NBP, KS, 2, 2>
                                                        : cim_fwd_v3_kernel<NBP, KS, 2, 4>;

@@ -68,8 +68,9 @@ def test_grad_scale_and_round_pass_values():
 
 
 def test_plain_modules_host_flag_mirror():
-    """Conv2dLSQ / ActLSQ read init_state / signed once (no device sync per forward); a
-    load_state_dict and GradBucket.broadcast_from reset the mirror."""
+    """Conv2dLSQ / ActLSQ read init_state / signed once (no device sync per forward); any in-place
+    write to the buffers (load_state_dict, GradBucket.broadcast_from, torch DDP's per-forward buffer
+    broadcast) bumps their version counter and the mirror re-reads them."""
     from cim_quantization_amd._modules.lsq import ActLSQ, Conv2dLSQ
     act, conv = ActLSQ(nbits_a=4), Conv2dLSQ(4, 4, 3, nbits_w=4)
     assert act._flags() == [False, False] and conv._flags() == [False, False]
@@ -81,6 +82,7 @@ def test_plain_modules_host_flag_mirror():
     assert act._range() == (-8, 7)
     with torch.no_grad():
         conv.init_state.fill_(1)
-    assert conv._flags()[0] is False  # a direct buffer write needs the reset, as for Conv2dLSQCiM
-    conv._state_cache = None
-    assert conv._flags()[0] is True
+    assert conv._flags()[0] is True  # a direct in-place write is seen
+    with torch.no_grad():
+        act.signed.copy_(torch.zeros_like(act.signed))  # what DDP's broadcast from rank 0 does
+    assert act._flags() == [True, False] and act._range() == (0, 15)

@@ -23,6 +23,12 @@ sys.path.insert(0, REPO)
 # DESIGN.md section 4.
 VARIANTS = {
     "base": [],
+    # round 4: the fused backward (cimq_fused.hip) and the first conv's (cimq_c1.hip)
+    "f_nogx": ["CIMQ_EXP_F_NOGX"],
+    "f_nogw": ["CIMQ_EXP_F_NOGW"],
+    "f_nostage": ["CIMQ_EXP_F_NOSTAGE"],
+    "f_nogxgw": ["CIMQ_EXP_F_NOGX", "CIMQ_EXP_F_NOGW"],
+    "c1_nopairs": ["CIMQ_EXP_C1_NOPAIRS"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
