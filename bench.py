@@ -40,7 +40,10 @@ PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward runs bf16 x3
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
 PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD-32 x 2.4 GHz (a wave64 VALU op issues over 2 cycles)
-TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r04", "pmc_traffic.json"))
+# grad_w + the parameter-gradient epilogue on a second stream (CIMQ_BENCH_OVERLAP=0: one stream,
+# the epilogues chained into the next layer's grad_x launch)
+OVERLAP = os.environ.get("CIMQ_BENCH_OVERLAP", "0") == "1"
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r04_final", "pmc_traffic.json"))
 # the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
 # prefixes (the keys of pmc_traffic.json); every launch of a family is timed, all its instantiations
 FAMILIES = {"fwd_v7": "cimq::cim_fwd_v3_kernel<", "bwd_fused": "cimq::cim_bwd_fused_kernel<",
@@ -85,10 +88,9 @@ class Trainer:
         from cim_quantization_amd.dist import GradBucket
         self.layers, self.world = layers, world
         self.bucket = GradBucket([p for m in layers for p in m.parameters()])  # one all-reduce per step
-        # the layers add their grads straight into the bucket.  (own(overlap=True) would run their
-        # parameter-gradient epilogues on a second stream: in the HIP graph that costs more in
-        # cross-queue edges than it hides, 3.60 -> 3.77 ms/step)
-        self.bucket.own(layers)
+        # the layers add their grads straight into the bucket; with OVERLAP their parameter-gradient
+        # half (grad_w + epilogue) runs on the bucket's second stream (GradBucket.own(overlap=True))
+        self.bucket.own(layers, overlap=OVERLAP)
         # DDP's construction-time broadcast; the step sizes are re-sent once more after the
         # first (initialising) step -- cim_quantization_amd/dist.py, DESIGN.md section 5
         self.bucket.broadcast_from(0, layers)

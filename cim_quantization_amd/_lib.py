@@ -13,12 +13,13 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
 CIMQ_LSQ_ACCUMULATE_GRADS = 1
 CIMQ_LSQ_SKIP_TAIL = 2
+CIMQ_LSQ_DEFER_GW = 4
 # cimq_conv_desc.adc_variant (include/cimq.h)
 CIMQ_ADC_LIBRARY = 0
 CIMQ_ADC_STOCHASTIC = 1
@@ -37,6 +38,7 @@ EXPORTED_SYMBOLS = (
     "cimq_module_forward",
     "cimq_module_backward",
     "cimq_module_backward_tail",
+    "cimq_module_backward_params",
     "cimq_module_backward_chain",
     "cimq_pending_flush",
     "cimq_module_prepare",
@@ -158,6 +160,8 @@ def _bind(lib):
     lib.cimq_module_backward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 16
     lib.cimq_module_backward_tail.restype = ctypes.c_int
     lib.cimq_module_backward_tail.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 9
+    lib.cimq_module_backward_params.restype = ctypes.c_int
+    lib.cimq_module_backward_params.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 10
     lib.cimq_module_backward_chain.restype = ctypes.c_int
     lib.cimq_module_backward_chain.argtypes = ([ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 15 +
                                                [ctypes.POINTER(Pending), _VP])

@@ -66,9 +66,19 @@ static Carry no_carry() {
 
 // carry: a previous layer's finish to run inside the v7 grad_x launch (struct Carry); only the v7
 // path can carry, so callers check v7_plan(g).ok before passing a non-empty one
+// layers whose backward is the separate v7 grad_x / grad_w pair: with CIMQ_LSQ_DEFER_GW the grad_w
+// kernel leaves cimq_module_backward for cimq_module_backward_params (the fused / first-conv kernels
+// and the general paths produce both in one pass)
+static bool gw_deferrable(const Geo& g) {
+  return g.variant == VAR_LIBRARY && v7_bwd(g) && !c1_plan(g).ok && !v9_plan(g).ok;
+}
+
+// parts: bit 0 grad_x (with everything a single-pass backward produces), bit 1 the deferred grad_w
+// kernel of a gw_deferrable layer
 int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                      const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused,
-                     const Carry& carry = no_carry()) {
+                     const Carry& carry = no_carry(), int parts = 3) {
+  if (parts == 2 && !gw_deferrable(g)) return fail(CIMQ_EINVAL, "internal: grad_w alone on a single-pass backward");
   if (!v7_bwd(g)) {
     if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
     if (dense_plan(g)) {
@@ -93,9 +103,9 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
   if (p7.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
-    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
-    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
-    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
   }
   if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
   if (dense_plan(g)) {
@@ -413,7 +423,7 @@ static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   a->gs_w = q->gscale_w;
   a->nbits_alpha = q->nbits_alpha;
   a->nalpha = g.T * g.nbw * g.nba * g.O;
-  if (q->flags & ~(CIMQ_LSQ_ACCUMULATE_GRADS | CIMQ_LSQ_SKIP_TAIL))
+  if (q->flags & ~(CIMQ_LSQ_ACCUMULATE_GRADS | CIMQ_LSQ_SKIP_TAIL | CIMQ_LSQ_DEFER_GW))
     return fail(CIMQ_EINVAL, "unknown LSQ flags 0x%x", q->flags);
   return CIMQ_OK;
 }
@@ -602,7 +612,8 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
     }
   }
   bool lsq_fused = false;
-  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused, carry));
+  const bool defer = (q->flags & CIMQ_LSQ_DEFER_GW) && gw_deferrable(g);
+  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused, carry, defer ? 1 : 3));
   // the act-LSQ partials: fused into the fast grad_x kernel, a separate pass otherwise
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
@@ -627,7 +638,8 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
     pend->magic = kPendingMagic;
     return CIMQ_OK;
   }
-  if (q->flags & CIMQ_LSQ_SKIP_TAIL) return CIMQ_OK;  // the caller runs cimq_module_backward_tail
+  // the caller runs cimq_module_backward_tail / _params
+  if (q->flags & (CIMQ_LSQ_SKIP_TAIL | CIMQ_LSQ_DEFER_GW)) return CIMQ_OK;
   return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
                      grad_alpha_cim, s);
 }
@@ -651,7 +663,8 @@ int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
   if (!pending) return fail(CIMQ_EINVAL, "null cimq_pending");
   Pending* pd = reinterpret_cast<Pending*>(pending);
   if (pd->magic != 0 && pd->magic != kPendingMagic) return fail(CIMQ_EINVAL, "cimq_pending not initialised (zero it)");
-  if (q && (q->flags & CIMQ_LSQ_SKIP_TAIL)) return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL with the chained backward");
+  if (q && (q->flags & (CIMQ_LSQ_SKIP_TAIL | CIMQ_LSQ_DEFER_GW)))
+    return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL / _DEFER_GW with the chained backward");
   return module_backward_impl(d, q, grad_out, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act,
                               ctx, grad_x, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim, ws, pd,
                               stream);
@@ -681,6 +694,35 @@ int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, c
                      reinterpret_cast<hipStream_t>(stream));
 }
 
+int cimq_module_backward_params(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                                const float* weight, const float* alpha_cim, const void* ctx, float* grad_weight,
+                                float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
+                                void* stream) {
+  Geo g;
+  LsqArgs la;
+  CIMQ_TRY(module_geo(d, q, &g, &la));
+  if (!(q->flags & CIMQ_LSQ_DEFER_GW)) return fail(CIMQ_EINVAL, "cimq_module_backward_params needs CIMQ_LSQ_DEFER_GW");
+  if (!grad_out || !weight || !ctx || !grad_weight || !grad_alpha_act || !grad_alpha_weight || !ws)
+    return fail(CIMQ_EINVAL, "null pointer argument");
+  const bool has_alpha = g.mode == ADC_SIGN || g.mode == ADC_TERNARY;
+  if (has_alpha && (!alpha_cim || !grad_alpha_cim || la.nbits_alpha == 0))
+    return fail(CIMQ_EINVAL, "adc 1 / 1.5 need alpha_cim and grad_alpha_cim");
+  if (!has_alpha) la.nbits_alpha = 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  if (gw_deferrable(g)) {
+    // the grad_w kernel cimq_module_backward left out (grad_out NCHW, as the v7 path reads it there)
+    g.onchw = 1;
+    const float* scal = reinterpret_cast<const float*>(wreg(g, c) + ctx_layout(g).lsq_scal);
+    bool lsq_fused = false;
+    CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, nullptr, grad_out, nullptr, nullptr, w, s, &lsq_fused,
+                              no_carry(), 2));
+  }
+  return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                     grad_alpha_cim, s);
+}
+
 int cimq_module_shift_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
                                const float* x, const float* weight, const float* alpha_act,
                                const float* alpha_weight, const float* alpha_cim, const float* beta_cim,
@@ -695,7 +737,8 @@ int cimq_module_shift_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
       !grad_alpha_act || !grad_alpha_weight || !grad_alpha_cim || !grad_beta_cim || !ws)
     return fail(CIMQ_EINVAL, "null pointer argument");
   if (la.nbits_alpha == 0) return fail(CIMQ_EINVAL, "the shift ADC needs alpha_cim (nbits_alpha > 0)");
-  if (q->flags & CIMQ_LSQ_SKIP_TAIL) return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL with cimq_module_shift_backward");
+  if (q->flags & (CIMQ_LSQ_SKIP_TAIL | CIMQ_LSQ_DEFER_GW))
+    return fail(CIMQ_EINVAL, "CIMQ_LSQ_SKIP_TAIL / _DEFER_GW with cimq_module_shift_backward");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
   uint8_t* w = reinterpret_cast<uint8_t*>(ws);

@@ -1,6 +1,8 @@
 // cimq_v7_launch.h -- launch sequence of the v7 backward (cim_bwd_gx_v8_kernel +
 // cim_bwd_gw_v7_kernel, cimq_v7.hip) as a template over the slice-pair shape; each shape is
 // instantiated in its own translation unit (cimq_part_v7_*.hip) so they compile in parallel.
+// parts: bit 0 the grad_x kernel, bit 1 the grad_w kernel (CIMQ_LSQ_DEFER_GW launches them apart,
+// grad_w on the caller's second stream).
 #pragma once
 #include "cimq_host.h"
 
@@ -9,12 +11,12 @@ namespace cimq {
 template <int NBW, int NBA, int OBX>
 int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                  const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
-                 const Carry& carry) {
+                 const Carry& carry, int parts) {
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
-  {
+  if (parts & 1) {
     const int np = p.v.NPART;
 #define CIMQ_GX8(L, S, N) cim_bwd_gx_v8_kernel<NBW, NBA, OBX, L, S, N>
 #ifdef CIMQ_TUNING
@@ -33,7 +35,7 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
     prof_end(slot, s);
     CIMQ_TRY(check_hip("cim_bwd_gx_v8"));
   }
-  {
+  if (parts & 2) {
     auto kern = g.SH == 1 ? cim_bwd_gw_v7_kernel<NBW, NBA, 1> : cim_bwd_gw_v7_kernel<NBW, NBA, 2>;
     CIMQ_TRY(set_lds(kern, p.lds_gw));
     const int slot = prof_begin(KID_GW_V7, g, s);
@@ -48,13 +50,13 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
 template <int NBW, int NBA>
 int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
-                const Carry& carry) {
+                const Carry& carry, int parts) {
   if constexpr (NBW * NBA > 10) {
-    return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);  // v7_plan: OB16 == 1
+    return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);  // v7_plan: OB16 == 1
   } else {
-    if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
-    if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
-    return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
   }
 }
 

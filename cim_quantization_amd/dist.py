@@ -67,10 +67,11 @@ class GradBucket:
         inside libcimq (no per-parameter AccumulateGrad kernels).  Only for parameters whose
         gradients the bucket exchanges itself: parameter hooks do not see those gradients.
 
-        ``overlap``: the layers run their parameter-gradient epilogue (slab reductions, quantiser
-        backward, step-size gradients) on the bucket's own stream, off the grad_x chain -- the
-        backward of the previous layer proceeds meanwhile.  ``join()`` (called by ``exchange()``)
-        orders the current stream after it; read the gradients only after that."""
+        ``overlap``: the layers run their parameter-gradient half -- the grad_w kernel where it is
+        one of its own (CIMQ_LSQ_DEFER_GW), then the epilogue (slab reductions, quantiser backward,
+        step-size gradients) -- on the bucket's own stream, off the grad_x chain: the backward of
+        the previous layer proceeds meanwhile.  ``join()`` (called by ``exchange()``) orders the
+        current stream after it; read the gradients only after that."""
         mine = {id(p) for p in self.params}
         if overlap and self.side is None and self.flat.is_cuda:
             self.side = torch.cuda.Stream(self.flat.device)

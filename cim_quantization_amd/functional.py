@@ -564,7 +564,7 @@ class _CimModuleConv(torch.autograd.Function):
         if targets is not None:
             gw, gaa, gaw, gac = targets
             lsq = _lib.make_lsq_desc(lsq.qn_w, lsq.qp_w, lsq.gscale_a, lsq.gscale_w, lsq.nbits_alpha,
-                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS | (_lib.CIMQ_LSQ_SKIP_TAIL if side else 0),
+                                     _lib.CIMQ_LSQ_ACCUMULATE_GRADS | (_lib.CIMQ_LSQ_DEFER_GW if side else 0),
                                      lsq.wprep)
         else:
             gw = torch.empty_like(wc)
@@ -600,16 +600,17 @@ class _CimModuleConv(torch.autograd.Function):
                                             None if gac is None else gac.data_ptr(), ws.data_ptr(), _stream()),
                    "cimq_module_backward")
         if side is not None:
-            # parameter-gradient epilogue on the bucket's stream: the next layer's backward does not
-            # wait for it; ws / ctx stay alive until that stream is done with them
+            # the parameter-gradient half (the grad_w kernel of the v7 layers, then the epilogue) on
+            # the bucket's stream: the next layer's backward does not wait for it; grad_out / ws /
+            # ctx stay alive until that stream is done with them
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                _lib.check(lib.cimq_module_backward_tail(ctx.desc, lsq, wc.data_ptr(),
-                                                         None if ac is None else ac.data_ptr(), cbuf.data_ptr(),
-                                                         gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
-                                                         None if gac is None else gac.data_ptr(), ws.data_ptr(),
-                                                         side.cuda_stream), "cimq_module_backward_tail")
-            for t in (ws, cbuf, wc) + ((ac,) if ac is not None else ()) + \
+                _lib.check(lib.cimq_module_backward_params(ctx.desc, lsq, g.data_ptr(), wc.data_ptr(),
+                                                           None if ac is None else ac.data_ptr(), cbuf.data_ptr(),
+                                                           gw.data_ptr(), gaa.data_ptr(), gaw.data_ptr(),
+                                                           None if gac is None else gac.data_ptr(), ws.data_ptr(),
+                                                           side.cuda_stream), "cimq_module_backward_params")
+            for t in (g, ws, cbuf, wc) + ((ac,) if ac is not None else ()) + \
                     ((ctx.wprep_buf,) if ctx.wprep_buf is not None else ()):
                 t.record_stream(side)
         if targets is not None:

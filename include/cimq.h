@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 9
+#define CIMQ_ABI_VERSION 10
 
 /* status codes */
 #define CIMQ_OK 0
@@ -74,6 +74,10 @@ extern "C" {
                                        grad_w / grad_alpha partials (left in ws); the caller runs
                                        cimq_module_backward_tail later, e.g. on a second stream
                                        (the parameter gradients are off the grad_x chain) */
+#define CIMQ_LSQ_DEFER_GW 4         /* as SKIP_TAIL, and on layers whose grad_w is a kernel of its
+                                       own (the v7 pair) that kernel is left out too: the caller
+                                       runs cimq_module_backward_params (grad_w + the epilogue) on
+                                       a second stream ordered after cimq_module_backward.  Since ABI 10 */
 
 typedef struct cimq_conv_desc {
   int32_t batch, in_channels, in_h, in_w; /* B, C, H, W */
@@ -174,6 +178,16 @@ int cimq_module_backward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const 
 int cimq_module_backward_tail(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* weight,
                               const float* alpha_cim, const void* ctx, float* grad_weight, float* grad_alpha_act,
                               float* grad_alpha_weight, float* grad_alpha_cim, void* ws, void* stream);
+
+/* The parameter-gradient half of a cimq_module_backward run with CIMQ_LSQ_DEFER_GW: the grad_w
+ * kernel that call left out (if the layer has one of its own), then the epilogue of
+ * cimq_module_backward_tail.  grad_out, ctx and ws are that call's, unchanged; the stream must be
+ * ordered after it (grad_w reads only grad_out and the forward's state, so it overlaps the next
+ * layer's grad_x when it runs on a second stream).  q->flags as that call's.  Since ABI 10. */
+int cimq_module_backward_params(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
+                                const float* weight, const float* alpha_cim, const void* ctx, float* grad_weight,
+                                float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
+                                void* stream);
 
 /* cimq_module_forward / cimq_module_backward for Conv2dLSQCiM(adc_shift=True): the per-tile scale +
  * shift ADC clamp(round((u - beta) / alpha_q), -1, 1) * alpha_q + beta of
