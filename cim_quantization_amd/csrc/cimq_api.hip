@@ -82,8 +82,8 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
   if (!v7_bwd(g)) {
     if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
     if (dense_plan(g)) {
-      *lsq_fused = false;
-      return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s);
+      *lsq_fused = g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0;
+      return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s, *lsq_fused ? x : nullptr, sa);
     }
     return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
   }
@@ -109,8 +109,8 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
   }
   if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
   if (dense_plan(g)) {
-    *lsq_fused = false;
-    return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s);
+    *lsq_fused = g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0;
+    return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s, *lsq_fused ? x : nullptr, sa);
   }
   return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
 }
@@ -143,6 +143,7 @@ int act_parts(const Geo& g) {
     if (v9_plan(g).ok || c1_plan(g).ok) return g.B;
     return g.B * v7_plan(g).v.nbands;
   }
+  if (dense_plan(g) && g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0) return dense_lsq_parts(g);
   int grid = cdiv(g.Nin, 256);
   return grid > kLsqParts ? kLsqParts : grid;
 }
@@ -366,8 +367,12 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   a.pp = params_of(g, const_cast<uint8_t*>(c));
   a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
   a.nchunks = W.nchunks_bwd;
-  a.nwb = cdiv((long long)g.T * g.FBT * 16 * g.Opad, 64);
-  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, 64) : 0;
+  // few chunks and many outputs (the dense path's 8 chunks of a 1024 x 1024 layer): one output per
+  // thread (16 k blocks of 64 outputs each took 67 us for 34 MB of slab)
+  const long long nout_w = (long long)g.T * g.FBT * 16 * g.Opad;
+  a.wide = (a.nchunks <= 16 && nout_w >= (1 << 18) && tune("WIDE_SLAB", 1)) ? 1 : 0;
+  a.nwb = cdiv(nout_w, a.wide ? 1024 : 64);
+  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, a.wide ? 1024 : 64) : 0;
   a.napart = act_parts(g);
   a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
   a.gapart = (has_alpha && la.nalpha > kFinishInReg && tune("WIDE_TAIL", 1)) ? reinterpret_cast<float*>(w + W.gapart) : nullptr;

@@ -634,6 +634,12 @@ inline int dense_chunks(const Geo& g) {
   const int per = std::max(1, 512 / (g.T * ((g.O + 127) / 128)));
   return std::max(1, std::min(per, g.M / 256));
 }
+// the dense grad_x kernel's MFMA waves (8 per block), each leaving one act-LSQ partial when it runs
+// the quantiser's backward (0: that does not fit the partial buffer, the separate pass runs)
+inline int dense_lsq_parts(const Geo& g) {
+  const int n = (g.M / 128) * g.T * 8;
+  return n <= std::max(kLsqParts, g.B * g.H) ? n : 0;
+}
 inline int dense_rows_per_chunk(const Geo& g) {
   const int n = dense_chunks(g);
   return ((g.M + n - 1) / n + 31) / 32 * 32;
@@ -821,7 +827,8 @@ int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const 
                        const int8_t* bmask, uint8_t* ws, float* grad_alpha, float* grad_beta, hipStream_t s,
                        int accum_beta = 0);
 int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
-                     hipStream_t s);
+                     hipStream_t s,
+                     const float* x = nullptr, const float* sa = nullptr);
 // cimq_part_bwd.hip: backward of layers outside the v7 / dense plans (the general kernels)
 int launch_bwd_general(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                        const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused);

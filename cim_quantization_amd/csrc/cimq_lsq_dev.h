@@ -88,6 +88,8 @@ struct ModuleTail {
   float cgrad;    // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
   int nchunks, nwb, nga, napart, accum;
   int gaq_ready;  // d loss / d alpha_q already in gaq (the shift ADC's statistics kernel): no slab sums
+  int wide;       // few chunks, many outputs (the dense path): one output per thread of a 1024-thread
+                  // block (nwb / nga count such blocks), the chunks summed in order by that thread
 };
 // alpha_cim sizes the one-block epilogue keeps in registers (module_finish_block); larger ones
 // (the QuantLinear layers: T * nbw * nba * O = 131072 at 1024 -> 1024 w4a4) take the wide path:
@@ -97,12 +99,28 @@ constexpr int kFinishInReg = 8 * 1024;
 // grad_w slab sum -> G = d loss / d w_q, then through w_q = rp * sw, rp = round_pass(clamp(w / sw)):
 //   grad_weight = mask * (G * sw) / sw; per block the partial sums of G * rp (MulBackward,
 //   d/d sw) and of -grad_t1 * ((w / sw) / sw) (DivBackward wrt the divisor) -> wpart[2*blk].
+// the slab sum of one output over few chunks, in chunk order, up to 8 loads in flight
+__device__ inline float sum_chunks_serial(const float* __restrict__ slab, size_t stride, int nchunks, size_t idx) {
+  float v = 0.f;
+  int c = 0;
+  for (; c + 8 <= nchunks; c += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = slab[(size_t)(c + u) * stride + idx];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; c < nchunks; ++c) v += slab[(size_t)c * stride + idx];
+  return v;
+}
+
 __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const size_t rows = (size_t)g.T * g.FBT * 16;
   const size_t nout = rows * g.Opad;
-  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
-  const int sub = threadIdx.x >> 6;
-  const float vsum = reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+  const size_t idx = a.wide ? (size_t)blk * blockDim.x + threadIdx.x : (size_t)blk * 64 + (threadIdx.x & 63);
+  const int sub = a.wide ? 0 : threadIdx.x >> 6;
+  const float vsum = a.wide ? (idx < nout ? sum_chunks_serial(a.gw_slab, nout, a.nchunks, idx) : 0.f)
+                            : reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
   float p_mul = 0.f, p_div = 0.f;
   if (sub == 0 && idx < nout) {
     const int o = (int)(idx % g.Opad);
@@ -125,6 +143,14 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
       p_div = -grad_t1 * (t1 / sw);
     }
   }
+  if (a.wide) {  // every thread holds an output: a block reduction
+    const float4 r = block_sum4(make_float4(p_mul, p_div, 0.f, 0.f), red);
+    if (threadIdx.x == 0) {
+      a.wpart[2 * blk] = r.x;
+      a.wpart[2 * blk + 1] = r.y;
+    }
+    return;
+  }
   // both partials live in the first wave only: a butterfly there, no block barriers
   if (sub == 0) {
 #pragma unroll
@@ -142,9 +168,11 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
 __device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const int nkj = g.nbw * g.nba;
   const size_t nout = (size_t)g.T * nkj * g.Opad;
-  const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
-  const float s = a.gaq_ready ? 0.f : reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  if ((threadIdx.x >> 6) != 0) return;
+  const size_t idx = a.wide ? (size_t)blk * blockDim.x + threadIdx.x : (size_t)blk * 64 + (threadIdx.x & 63);
+  const float s = a.gaq_ready ? 0.f
+                  : a.wide ? (idx < nout ? sum_chunks_serial(a.ga_slab, nout, a.nchunks, idx) : 0.f)
+                           : reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+  if (!a.wide && (threadIdx.x >> 6) != 0) return;
   float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
   if (idx < nout) {
     const int o = (int)(idx % g.Opad);
@@ -175,7 +203,10 @@ __device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleT
       }
     }
   }
-  if (a.gapart) {
+  if (a.gapart && a.wide) {
+    const float4 r = block_sum4(part, red);
+    if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = r;
+  } else if (a.gapart) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       part.x += __shfl_xor(part.x, off);

@@ -226,7 +226,9 @@ __global__ __launch_bounds__(256) void dense_fwd_lit_kernel(Geo g, const uint8_t
 template <int NBW, int NBA>
 __global__ __launch_bounds__(1024) void dense_gx_kernel(Geo g, const uint2* __restrict__ st, const v4i* __restrict__ wgx,
                                                         Params pp, const float* __restrict__ sw_p,
-                                                        const float* __restrict__ gout, float* __restrict__ gx) {
+                                                        const float* __restrict__ gout, float* __restrict__ gx,
+                                                        const float* __restrict__ x, const float* __restrict__ sa_p,
+                                                        float* __restrict__ gsa_part) {
   constexpr int NKJ = NBW * NBA;
   __shared__ v4i Gs[2 * 3 * 8 * 64];  // [buffer][hi/mid/lo][16-row block][lane]
   __shared__ float cel[NKJ];
@@ -338,6 +340,11 @@ __global__ __launch_bounds__(1024) void dense_gx_kernel(Geo g, const uint2* __re
     for (int f = 0; f < 4; ++f) bc[f] = bn[f];
   }
   const float scale = *sw_p / (float)NBA;
+  // with x: the LSQ activation quantiser's backward fused into the store (as lsq_act_bwd_kernel,
+  // the same operations: autograd of round_pass(clamp(x / sa, 0, Qp)) * sa, lsq.py:549) and this
+  // block's partial of d loss / d sa
+  const float sa = x ? *sa_p : 1.f;
+  float gsum = 0.f;
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     if (f >= nf) break;
@@ -346,8 +353,28 @@ __global__ __launch_bounds__(1024) void dense_gx_kernel(Geo g, const uint2* __re
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gx[((size_t)m0 + 32 * rg + 16 * h + 4 * g4 + r) * g.C + c] = acc[h][f][r] * scale;
+        for (int r = 0; r < 4; ++r) {
+          const size_t e = ((size_t)m0 + 32 * rg + 16 * h + 4 * g4 + r) * g.C + c;
+          const float gq = acc[h][f][r] * scale;
+          if (x) {
+            const float y1 = x[e] / sa;
+            const float cl = clamp_nan(y1, 0.f, g.lsq_qp);
+            const float rr = rintf(cl);
+            const float rp = (rr - cl) + cl;
+            const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
+            const float gy = pass ? gq * sa : 0.f;
+            gx[e] = gy / sa;
+            gsum += gq * rp;
+            gsum += -(gy * (y1 / sa));
+          } else {
+            gx[e] = gq;
+          }
+        }
     }
+  }
+  if (x) {  // one partial per MFMA wave (the builder waves have returned: no block barrier here)
+    for (int o = 32; o > 0; o >>= 1) gsum += __shfl_xor(gsum, o);
+    if (lane == 0) gsa_part[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + wave] = gsum;
   }
 }
 
@@ -518,7 +545,7 @@ int launch_dense_fwd_n(const Geo& g, uint8_t* ctx, const float* sw, const float*
 
 template <int NBW, int NBA>
 int launch_dense_bwd_n(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
-                       hipStream_t s) {
+                       hipStream_t s, const float* x, const float* sa) {
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
@@ -526,7 +553,8 @@ int launch_dense_bwd_n(const Geo& g, const uint8_t* ctx, const float* sw, const 
   {
     const int slot = prof_begin(KID_BWD_GX, g, s);
     hipLaunchKernelGGL((dense_gx_kernel<NBW, NBA>), dim3(g.M / 128, g.T), dim3(1024), 0, s, g, st,
-                       reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wgx), pp, sw, gout, gx);
+                       reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wgx), pp, sw, gout, gx, x, sa,
+                       reinterpret_cast<float*>(ws + W.lsq_part));
     prof_end(slot, s);
     CIMQ_TRY(check_hip("dense_gx"));
   }
@@ -555,8 +583,8 @@ int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* s
 }
 
 int launch_dense_bwd(const Geo& g, const uint8_t* ctx, const float* sw, const float* gout, float* gx, uint8_t* ws,
-                     hipStream_t s) {
-  CIMQ_DENSE_SEL(launch_dense_bwd_n, g, ctx, sw, gout, gx, ws, s)
+                     hipStream_t s, const float* x, const float* sa) {
+  CIMQ_DENSE_SEL(launch_dense_bwd_n, g, ctx, sw, gout, gx, ws, s, x, sa)
 }
 
 }  // namespace cimq
