@@ -1,6 +1,7 @@
-"""GPU parity of BASELINE cfg4's scale + shift ADC (Conv2dLSQCiM(adc_shift=True), the per-tile
-partial-sum scale/shift of test/test_backward_cimlayer_scale_shift.py:336-546 as a module option) on
-the FULL batch, and on the layers outside the shift fast path.
+"""GPU parity of BASELINE cfg4 (ResNet-56 w2a2 xbar 64) on the module path at full batch: the scale +
+shift ADC (Conv2dLSQCiM(adc_shift=True), the per-tile partial-sum scale/shift of
+test/test_backward_cimlayer_scale_shift.py:336-546 as a module option), alpha only (the reference
+module, lsq.py:511-588), and the layers outside the shift fast path.
 
 * ResNet-56 w2a2 xbar 64 at B = 256, every stage geometry and both stride-2 transitions: out, grad_x,
   grad_w, grad_alpha_cim, grad_beta and both step-size gradients against the module oracle on the
@@ -9,6 +10,7 @@ the FULL batch, and on the layers outside the shift fast path.
   3 -> 16 @ 32, signed input, xbar 64 (K = 27, T = 1, 64 slice pairs, the int8-wrapped binary_mask),
   at B = 2 and B = 256.  It is off the shift fast path (which takes 2 or 3 equal slices): the general
   recompute kernels, deterministic (fixed-order reductions, no atomics).
+* alpha only (adc_shift=False) at B = 256: the 32x32 stage, a stride-2 transition and the 8x8 stage.
 * Shift layers the fast path refuses for other reasons: 128 output channels (more than four 16-channel
   blocks) and a batch-1 8x8 image (M % 128 != 0).
 
@@ -31,9 +33,9 @@ from oracle import cim_oracle as co
 pytestmark = pytest.mark.gpu
 
 
-def _kw(bits, xbar=64):
+def _kw(bits, xbar=64, shift=True):
     return dict(nbits_w=bits, nbits_a=bits, nbits_alpha=8, wbitslice=1, abitslice=1, xbar=xbar, adcbits=1.5,
-                stochastic_quant=False, adc_shift=True)
+                stochastic_quant=False, adc_shift=shift)
 
 
 def _capture_oracle_ctx(monkeypatch):
@@ -57,14 +59,14 @@ def _scalar_terms(x, g_xq, s, qn, qp, gscale):
     return gscale * (np.abs(g * r).sum() + np.abs(np.where(inside, g * float(s), 0) * y / float(s)).sum())
 
 
-def _build(dev, C, O, H, s, bits, B, seed, signed):
+def _build(dev, C, O, H, s, bits, B, seed, signed, shift=True):
     """The MI355X module and the oracle module with identical weights and step sizes; alpha_cim from
     the reference's data-driven init (lsq.py:557-563) on a few images, spread so codes vary; beta a
     fraction of alpha of either sign."""
     import cim_quantization_amd._modules as my_nn
     rng = np.random.default_rng(seed)
-    m = my_nn.Conv2dLSQCiM(C, O, (3, 3), (s, s), (1, 1), (1, 1), bias=False, **_kw(bits)).to(dev)
-    om = cmo.OracleConv2dLSQCiM(C, O, (3, 3), (s, s), (1, 1), (1, 1), bias=False, **_kw(bits))
+    m = my_nn.Conv2dLSQCiM(C, O, (3, 3), (s, s), (1, 1), (1, 1), bias=False, **_kw(bits, shift=shift)).to(dev)
+    om = cmo.OracleConv2dLSQCiM(C, O, (3, 3), (s, s), (1, 1), (1, 1), bias=False, **_kw(bits, shift=shift))
     om.debug_retain = True
     w = (rng.standard_normal((O, C, 3, 3)) * math.sqrt(2.0 / (9 * C))).astype(np.float32)
     x = rng.standard_normal((B, C, H, H)).astype(np.float32)
@@ -86,7 +88,8 @@ def _build(dev, C, O, H, s, bits, B, seed, signed):
             mod.alpha_act.fill_(float(aa))
             mod.alpha_weight.fill_(float(aw))
             mod.alpha_cim.copy_(torch.from_numpy(ac))
-            mod.beta_cim.copy_(torch.from_numpy(bc))
+            if shift:
+                mod.beta_cim.copy_(torch.from_numpy(bc))
             mod.init_state.fill_(1)
             mod.init_state_cim.fill_(1)
             mod.signed_act.fill_(1 if signed else 0)
@@ -105,11 +108,12 @@ def _run(m, x, g, dev):
     out.backward(torch.from_numpy(g).to(dev))
     torch.cuda.synchronize()
     return dict(out=out.detach().clone(), gx=xt.grad.clone(), gw=m.weight.grad.clone(), ga=m.alpha_cim.grad.clone(),
-                gb=m.beta_cim.grad.clone(), gaa=m.alpha_act.grad.clone(), gaw=m.alpha_weight.grad.clone())
+                gb=m.beta_cim.grad.clone() if m.beta_cim is not None else torch.zeros(1, device=dev),
+                gaa=m.alpha_act.grad.clone(), gaw=m.alpha_weight.grad.clone())
 
 
-def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True):
-    m, om, x, w, g, qp_a, qn_w, qp_w = _build(dev, C, O, H, s, bits, B, seed, signed)
+def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True, shift=True):
+    m, om, x, w, g, qp_a, qn_w, qp_w = _build(dev, C, O, H, s, bits, B, seed, signed, shift)
     r1 = _run(m, x, g, dev)
     if repeat:
         r2 = _run(m, x, g, dev)
@@ -122,14 +126,16 @@ def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True):
     c = box["c"]
     ho = g.shape[-1]
     g_bpo = np.ascontiguousarray(g.reshape(B, O, ho * ho).transpose(0, 2, 1))
-    ax, aw, aa, ab = co.cim_backward(c, g_bpo, absolute=True)
+    terms = co.cim_backward(c, g_bpo, absolute=True)
+    ax, aw, aa = terms[:3]
     bm = np.abs(om.binary_mask.numpy().astype(np.float64))
     out_terms = (np.abs(c.adc.astype(np.float64)) * bm).sum(axis=(1, 2, 3)).transpose(0, 2, 1).reshape(B, O, ho, ho)
     np_ = lambda t: t.detach().cpu().numpy()  # noqa: E731
     assert rel_err(np_(r1["out"]), np_(oout), out_terms) < 1e-6, "out"
     assert rel_err(np_(r1["gx"]), np_(ox.grad), ax) < 1e-5, "grad_x"
     assert rel_err(np_(r1["gw"]), np_(om.weight.grad), aw.reshape(om.weight.shape)) < 1e-5, "grad_w"
-    assert rel_err(np_(r1["gb"]), np_(om.beta_cim.grad), ab.reshape(om.beta_cim.shape)) < 1e-5, "grad_beta"
+    if shift:
+        assert rel_err(np_(r1["gb"]), np_(om.beta_cim.grad), terms[3].reshape(om.beta_cim.shape)) < 1e-5, "grad_beta"
     ga, gr = np_(r1["ga"]), np_(om.alpha_cim.grad)
     a = np_(om.alpha_cim)
     inner = (a != a.max()) & (a != a.min())
@@ -152,7 +158,8 @@ def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True):
     assert abs(r1["gaw"].item() - om.alpha_weight.grad.item()) <= 1e-5 * t_w, "grad_alpha_weight"
     # the check must bite: partial sums inside and outside the STE interval, codes of either sign
     with np.errstate(all="ignore"):
-        v = (c.u.astype(np.float64) - c.beta.astype(np.float64)) / c.alpha.astype(np.float64)
+        be = c.beta.astype(np.float64) if c.beta is not None else 0.0
+        v = (c.u.astype(np.float64) - be) / c.alpha.astype(np.float64)
     assert (np.abs(v) >= 1 + 1e-5).mean() > 0.01 and (np.abs(v) < 1).mean() > 0.01
     assert (np.rint(v) > 0).any() and (np.rint(v) < 0).any()
     return m
@@ -181,3 +188,12 @@ def test_shift_off_fast_path_vs_oracle(cuda_device, monkeypatch, C, O, H, s, B):
     M % 128 != 0): the general backward, with grad_beta, the shift ADC's grad_alpha and the act-LSQ
     backward applied once."""
     _check(cuda_device, monkeypatch, C, O, H, s, 2, B, 9300 + C + O + H + B, signed=False)
+
+
+@pytest.mark.parametrize("C,O,H,s", [(16, 16, 32, 1), (16, 32, 32, 2), (64, 64, 8, 1)])
+def test_resnet56_alpha_only_fullbatch_vs_oracle(cuda_device, monkeypatch, C, O, H, s):
+    """BASELINE cfg4 without the shift option: Conv2dLSQCiM w2a2 xbar 64, alpha only (lsq.py:511-588),
+    on the module path at ResNet-56's 32x32 geometry (and a stride-2 transition and an 8x8 stage),
+    B = 256: out, grad_x, grad_w, grad_alpha_cim and both step sizes against the module oracle on the
+    whole batch, elementwise, plus run-to-run bit identity."""
+    _check(cuda_device, monkeypatch, C, O, H, s, 2, 256, 9400 + C + O + H + s, signed=False, shift=False)
