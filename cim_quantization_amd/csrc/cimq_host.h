@@ -648,7 +648,10 @@ inline int dense_rows_per_chunk(const Geo& g) {
 // the shift ADC's statistics kernel (cimq_part_shift.hip) applies: interleaved 3-bit state words of
 // w2a2 / w3a3 on a v7 shape (other shift layers take the general backward)
 inline bool shift_stats_ok(const Geo& g) {
-  return shift_fast(g) && g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
+  if (!shift_fast(g)) return false;
+  if (g.NBP == 8)  // the w8a8 first conv: one K-step, one crossbar tile (shift_stats8_kernel)
+    return g.nbw == 8 && g.nba == 8 && g.KS == 1 && g.T == 1 && g.bsw == 1 && g.bsa == 1;
+  return g.NBP == 4 && g.nbw == g.nba && (g.nbw == 2 || g.nbw == 3);
 }
 // half-range of its q tables: the largest |ps| of 0 .. 2^bs - 1 slices over one tile (the sign slice of
 // the weights included); larger partial sums (slice artifacts) take the direct evaluation

@@ -162,6 +162,116 @@ __global__ __launch_bounds__(256) void shift_stats_kernel(Geo g, V3 v, const uin
   }
 }
 
+// The w8a8 first conv under the shift ADC (K <= 32: one K-step, 64 slice pairs, 36 live under the
+// int8-wrapped mask): the same sums with slice k a rolled loop (eight live accumulator pairs at a time;
+// a full unroll of the 64 pairs would hold 128 of them), q evaluated directly (its table, 64 pairs x
+// 16 channels x 55 partial sums, exceeds LDS), and each slice's sums folded over the four pixel rows of
+// a lane by half-wave swaps into the wave's LDS region -- still a fixed order, no atomics.
+__global__ __launch_bounds__(256) void shift_stats8_kernel(Geo g, V3 v, const uint8_t* __restrict__ xcf,
+                                                           const v4i* __restrict__ wfrag, Params pp,
+                                                           const float* __restrict__ sw_p,
+                                                           const float* __restrict__ sa_p,
+                                                           const float* __restrict__ gout, float* __restrict__ slab,
+                                                           int nsc) {
+  constexpr int NS = 8, NKJ = 64, NBP = 8;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int i = blockIdx.y / g.OB16, ob = blockIdx.y - i * g.OB16;
+  const int c_lo = (i * g.xbar) / g.KHW, c_hi = (min(g.K, (i + 1) * g.xbar) - 1) / g.KHW;
+  const int ncx = c_hi - c_lo + 1;
+  uint8_t* cur = smem;
+  float* red = reinterpret_cast<float*>(cur); cur += (size_t)4 * 2 * NKJ * 16 * 4;   // [wave][q | c][kj][16]
+  float2* abl = reinterpret_cast<float2*>(cur); cur += (size_t)NKJ * 16 * 8;          // alpha, beta [kj][16]
+  v4i* wkl = reinterpret_cast<v4i*>(cur); cur += (size_t)NS * 64 * 16;                // weight slices [k][lane]
+  int* ptab = reinterpret_cast<int*>(cur); cur += 64 * 4;
+  uint8_t* patch = cur;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int o = ob * 16 + r16;
+  const bool ov = o < g.O;
+  build_ptab(g, i, 1, v.RH, v.WP, ptab, c_lo);
+  zero_lds(reinterpret_cast<uint32_t*>(patch), ncx * v.RH * v.WP * NBP / 4);
+  for (int t = threadIdx.x; t < 4 * 2 * NKJ * 16; t += blockDim.x) red[t] = 0.f;
+  for (int t = threadIdx.x; t < NKJ * 16; t += blockDim.x) {
+    const int kj = t >> 4, col = t & 15, k = kj / NS, j = kj - k * NS;
+    const int oc = min(ob * 16 + col, g.O - 1);
+    abl[t] = make_float2(pp.alpha[pidx(g, i, j, k, oc)], pp.beta[pidx(g, i, j, k, oc)]);
+  }
+  for (int t = threadIdx.x; t < NS * 64; t += blockDim.x)
+    wkl[t] = wfrag[((size_t)i * g.NBLK + (t >> 6) * g.OB16 + ob) * WAVE + (t & 63)];
+  __syncthreads();
+  // pairs with a nonzero mask (the others add mask * sum = 0 in shift_combine_kernel)
+  const uint64_t live = __builtin_amdgcn_ballot_w64(pp.ckj[lane] != 0.f);
+  const float sw = *sw_p, sa = *sa_p;
+  const int Wo = 1 << v.lw;
+  const int pl = wave * 16 + r16;
+  const int rb = ((pl >> v.lw) * g.SH) * v.WP + (pl & (Wo - 1)) * g.SW;
+  const int tpi = g.P >> 6;
+  float* rq = red + (size_t)wave * 2 * NKJ * 16;
+  for (int mt = blockIdx.x; mt < v.nmt; mt += nsc) {
+    const int b = mt / tpi, p0 = (mt - b * tpi) * 64;
+    __syncthreads();
+    stage_rows<NBP>(g, v.WP, v.RH, xcf, b, (p0 >> v.lw) * g.SH - g.PH, patch, c_lo, ncx);
+    __syncthreads();
+    v4i xs[NBP][1];
+    gather_xs<NBP, 1>(patch, rb, ptab, g4, xs);
+    float gv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mt * 64 + wave * 16 + 4 * g4 + r;
+      const int pm = p0 + wave * 16 + 4 * g4 + r;
+      gv[r] = ov ? (g.onchw ? gout[((size_t)b * g.O + o) * g.P + pm] : gout[(size_t)m * g.O + o]) : 0.f;
+    }
+#pragma unroll 1
+    for (int k = 0; k < NS; ++k) {
+      const v4i wkk = wkl[k * 64 + lane];
+      const unsigned lk = (unsigned)(live >> (8 * k)) & 0xFFu;
+      float qs[NS], cs[NS];
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        qs[j] = cs[j] = 0.f;
+        if (!((lk >> j) & 1u)) continue;  // uniform
+        const v4i ps = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][0], wkk, v4i{0, 0, 0, 0}, 0, 0, 0);
+        const float2 ab = abl[(k * NS + j) * 16 + r16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float q = shift_q(ps[r], sw, sa, ab.x, ab.y, g.thr_hi, g.thr_lo);
+          qs[j] += q * gv[r];
+          cs[j] += (fabsf(q) == 1.f) ? gv[r] : 0.f;  // clamped: grad_beta's region
+        }
+      }
+      // the lane's four pixel rows -> every lane of the channel (two half-wave swaps), then lane row
+      // g4 adds pairs j = g4 and g4 + 4 of this slice to the wave's region
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        auto fold = [](float x) {
+          const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+          const float h = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+          const auto c = __builtin_amdgcn_permlane16_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+          return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+        };
+        qs[j] = fold(qs[j]);
+        cs[j] = fold(cs[j]);
+      }
+      const float q0 = g4 == 0 ? qs[0] : g4 == 1 ? qs[1] : g4 == 2 ? qs[2] : qs[3];
+      const float q1 = g4 == 0 ? qs[4] : g4 == 1 ? qs[5] : g4 == 2 ? qs[6] : qs[7];
+      const float c0 = g4 == 0 ? cs[0] : g4 == 1 ? cs[1] : g4 == 2 ? cs[2] : cs[3];
+      const float c1 = g4 == 0 ? cs[4] : g4 == 1 ? cs[5] : g4 == 2 ? cs[6] : cs[7];
+      float* d = rq + (k * NS + g4) * 16 + r16;
+      d[0] += q0;
+      d[4 * 16] += q1;
+      d[NKJ * 16] += c0;
+      d[NKJ * 16 + 4 * 16] += c1;
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * NKJ * 16; t += blockDim.x) {
+    const int w2 = 2 * NKJ * 16;
+    const float sum = (red[t] + red[w2 + t]) + (red[2 * w2 + t] + red[3 * w2 + t]);
+    const int which = t / (NKJ * 16), rem = t - which * NKJ * 16, kj = rem >> 4, col = rem & 15;
+    slab[(((size_t)blockIdx.x * g.T + i) * 2 + which) * NKJ * g.Opad + (size_t)kj * g.Opad + ob * 16 + col] = sum;
+  }
+}
+
 // fixed-order sum over the pixel chunks, times the binary mask: [1, T, nbw, nba, 1, O] each.  One wave
 // per output: lane l sums chunks l, l + 64, ..., then a fixed butterfly (deterministic)
 __global__ __launch_bounds__(256) void shift_combine_kernel(Geo g, const float* __restrict__ slab, int nsc,
@@ -210,10 +320,25 @@ int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const 
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   const int nsc = shift_chunks(g);
-  const bool lut = shift_table_fits(g);
-  const int R = shift_table_range(g);
   const int nkj = g.nbw * g.nba;
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
+  float* slab = reinterpret_cast<float*>(ws + W.ss_slab);
+  if (g.NBP == 8) {  // the w8a8 first conv (shift_stats_ok: one K-step)
+    const int ncx = (std::min(g.K, g.xbar) - 1) / g.KHW + 1;
+    const size_t lds = (size_t)4 * 2 * 64 * 16 * 4 + (size_t)64 * 16 * 8 + (size_t)8 * 64 * 16 + 64 * 4 +
+                       a16((size_t)ncx * p.v.RH * p.v.WP * 8);
+    CIMQ_TRY(set_lds(shift_stats8_kernel, lds));
+    hipLaunchKernelGGL(shift_stats8_kernel, dim3(nsc, g.T * g.OB16), dim3(256), lds, s, g, p.v, ctx + L.xcode,
+                       reinterpret_cast<const v4i*>(wreg(g, const_cast<uint8_t*>(ctx)) + L.wfrag), pp, sw, sa, gout,
+                       slab, nsc);
+    CIMQ_TRY(check_hip("shift_stats8"));
+    const int total = g.T * nkj * g.O;
+    hipLaunchKernelGGL(shift_combine_kernel, dim3(std::min(cdiv(total, 4), 2048)), dim3(256), 0, s, g, slab, nsc,
+                       bmask, grad_alpha, grad_beta, accum_beta);
+    return check_hip("shift_combine");
+  }
+  const bool lut = shift_table_fits(g);
+  const int R = shift_table_range(g);
   float* qtab = reinterpret_cast<float*>(ws + W.qtab);
   if (lut) {
     const long long nt = (long long)g.T * g.OB16 * nkj * 16 * (2 * R + 1);
@@ -234,7 +359,6 @@ int launch_shift_stats(const Geo& g, const uint8_t* ctx, const float* sw, const 
   else if (g.nbw == 2) kern = lut ? stats_ptr<2, 2, true>() : stats_ptr<2, 2, false>();
   else kern = lut ? stats_ptr<2, 3, true>() : stats_ptr<2, 3, false>();
   CIMQ_TRY(set_lds(kern, lds));
-  float* slab = reinterpret_cast<float*>(ws + W.ss_slab);
   hipLaunchKernelGGL(kern, dim3(nsc, g.T * g.OB16), dim3(256), lds, s, g, p.v, ctx + L.xcode,
                      reinterpret_cast<const v4i*>(wreg(g, const_cast<uint8_t*>(ctx)) + L.wfrag), pp, sw, sa, gout,
                      qtab, R, slab, nsc);
