@@ -329,7 +329,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   for (int i = 0; i < g.T; ++i) build_ptab(g, i, KS, v.RH, v.WP, ptab + i * KS * 64);
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
   if (v.fwd_res)
+#ifndef CIMQ_EXP_FWD_NOSTAGEW  // attribution builds only (tools/kernel_experiment.py)
     for (int i = 0; i < g.T; ++i) stage_tile(i, i);
+#endif
   zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * v.RH * v.WP * NBP / 4);
 
   __syncthreads();
@@ -345,7 +347,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     const int b = fdiv(mt, tiles_per_img, inv_tpi), p0 = (mt - b * tiles_per_img) * 64;
     const int oh0 = p0 >> v.lw;
     __syncthreads();
+#ifndef CIMQ_EXP_FWD_NOSTAGEX
     stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
+#endif
     __syncthreads();
     float acc[OBM][4];
 #pragma unroll
@@ -355,7 +359,9 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     for (int i = 0; i < g.T; ++i) {
       if (!v.fwd_res) {
         __syncthreads();
+#ifndef CIMQ_EXP_FWD_NOSTAGEW
         stage_tile(i, 0);
+#endif
         __syncthreads();
       }
       const int tt = v.fwd_res ? i : 0;

@@ -29,6 +29,10 @@ VARIANTS = {
     "f_nostage": ["CIMQ_EXP_F_NOSTAGE"],
     "f_nogxgw": ["CIMQ_EXP_F_NOGX", "CIMQ_EXP_F_NOGW"],
     "c1_nopairs": ["CIMQ_EXP_C1_NOPAIRS"],
+    # forward staging: the weight side (fragments + ADC parameters per tile) / the activation rows
+    "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],
+    "fwd_nostagex": ["CIMQ_EXP_FWD_NOSTAGEX"],
+    "fwd_nostage": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
