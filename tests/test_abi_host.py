@@ -137,9 +137,10 @@ def test_module_prepare_validates_items(lib):
 @pytest.mark.parametrize("C,O,H,s", [(16, 16, 32, 1), (32, 32, 16, 1), (64, 64, 8, 1), (16, 32, 32, 2),
                                      (32, 64, 16, 2)])
 def test_module_shift_supported_resnet56_shapes(lib, C, O, H, s):
-    """cfg4's Conv2dLSQCiM(adc_shift=True) layers (w2a2 xbar 64, adc 1.5) take the fused shift path;
-    the test scripts' variants (int8 ps buffer, shift range), the sign ADC, the w8a8 first layer and
-    non-RAW input do not (host plan only, no GPU call)."""
+    """cfg4's Conv2dLSQCiM(adc_shift=True) layers (w2a2 xbar 64, adc 1.5) and, since round 4, its w8a8
+    first conv (the plane-state backward + shift_stats8_kernel) take the fused shift path; the test
+    scripts' variants (int8 ps buffer, shift range), the sign ADC and non-RAW input do not (host plan
+    only, no GPU call)."""
     kw = dict(B=256, C=C, H=H, W=H, O=O, stride=(s, s), xbar=64, bits_w=2, bits_a=2,
               input_kind=L.CIMQ_INPUT_RAW_LSQ, lsq_qp=3.0)
     assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw)) == 1
@@ -149,6 +150,8 @@ def test_module_shift_supported_resnet56_shapes(lib, C, O, H, s):
     kw1 = dict(kw, adc_bits=1.0)
     assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_SIGN, **kw1)) == 0
     kw8 = dict(kw, C=3, O=16, H=32, W=32, stride=(1, 1), bits_w=8, bits_a=8, lsq_qp=255.0)
-    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw8)) == 0
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw8)) == 1
+    kw8w = dict(kw8, C=8)  # K = 72 > 64: two K-steps, off the w8a8 statistics kernel
+    assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw8w)) == 0
     kwx = dict(kw, input_kind=L.CIMQ_INPUT_XQ)
     assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kwx)) == 0
