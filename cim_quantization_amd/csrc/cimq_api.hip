@@ -510,6 +510,9 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
       nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.npp, 256), 1024));
     }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
+    if (fwd_actq_ok(g)) a.nact_blocks = 0;  // the forward's row staging quantises (stage_rows_q)
+    if (a.nact_blocks + nwblk == 0) goto prepared;
+    {
     const int slot = prof_begin(KID_PREP_ACT, g, s);
     ModulePrep aw = a;
     if (nwblk > 0 && has_alpha && la.nalpha > kFinishInReg && tune("WIDE_PREP", 1)) {  // wide alpha_cim: its max / min in 64 blocks first
@@ -521,11 +524,14 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
     hipLaunchKernelGGL(prep_module_kernel, dim3(a.nact_blocks + nwblk), dim3(256), 0, s, g, la, aw);
     prof_end(slot, s);
     CIMQ_TRY(check_hip("prep_module"));
+    }
   }
+prepared:
   const Plan3 p = v3_plan(g);
   if (p.ok) {
     g.onchw = 1;
-    return launch_fwd_any(g, c, scal + 1, scal, out, nullptr, nullptr, s);
+    const ActQ aq{x, signed_act};
+    return launch_fwd_any(g, c, scal + 1, scal, out, nullptr, nullptr, s, fwd_actq_ok(g) ? &aq : nullptr);
   }
   if (dense_plan(g)) return launch_fwd_any(g, c, scal + 1, scal, out, nullptr, nullptr, s);  // P = 1: NCHW is [B, P, O]
   // general kernels write [B, P, O]; the module returns NCHW

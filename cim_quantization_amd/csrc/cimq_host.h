@@ -665,8 +665,25 @@ inline bool shift_table_fits(const Geo& g) {
 
 // the backward runs on the v7 plan's state words (v7 / fused / first-conv kernels): the library ADC, or
 // the shift ADC where the statistics kernel takes it; every other layer runs the general kernels
+// the module forward with the LSQ activation quantiser fused into the forward's row staging: the
+// v3 fast path with v7 state words (so no later kernel reads the forward slice words), 4-byte slice
+// words, the prologue's word table applicable, and not the first conv (whose backward re-reads the
+// forward words) or a shift layer (its statistics kernel does)
+struct ActQ {
+  const float* x;
+  const float* signed_act;
+};
+inline bool v7_bwd(const Geo& g);
+inline bool fwd_actq_ok(const Geo& g);
+
 inline bool v7_bwd(const Geo& g) {
   return v7_plan(g).ok && (g.variant == VAR_LIBRARY || shift_stats_ok(g));
+}
+
+inline bool fwd_actq_ok(const Geo& g) {
+  if (tune("ACTQ", 1) == 0) return false;
+  return g.input_kind == CIMQ_INPUT_RAW_LSQ && g.NBP == 4 && g.variant == VAR_LIBRARY && g.W % 4 == 0 &&
+         g.P % 64 == 0 && g.lsq_qp >= 0.f && g.lsq_qp < 255.f && v3_plan(g).ok && v7_bwd(g) && !c1_plan(g).ok;
 }
 
 struct WsLayout {
@@ -821,7 +838,8 @@ inline void prof_end(int slot, hipStream_t s) {
 // cimq_part_fwd.hip: the forward partial-sum kernels (v3 fast path or the general kernel;
 // the general kernel with ps_dbg / adc_dbg also writes every partial sum and ADC output)
 int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
-                   float* adc_dbg, hipStream_t s);
+                   float* adc_dbg, hipStream_t s,
+                   const ActQ* aq = nullptr);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
 // shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words

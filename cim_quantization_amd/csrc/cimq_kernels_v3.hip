@@ -118,6 +118,81 @@ __device__ inline void stage_rows(const Geo& g, int WP, int RHx, const uint8_t* 
   }
 }
 
+// stage_rows for the module forward with the LSQ activation quantiser fused (NBP 4): the rows are read
+// as fp32 x and turned into slice words on the way into LDS -- act_words_lut, the same table and the
+// same element chain as the prologue's act_range, so the words are bit-identical -- and the block
+// that owns input rows [own_lo, own_hi) also writes their backward (ctx) words to xcb.  The forward
+// slice words are never stored.
+// lut: [Qp + 1][fwd, bwd] from act_lut_build plus, at entry Qp + 1, the words of a NaN element
+// (act_words of any NaN: every step of its chain is independent of the NaN's sign and payload)
+__device__ inline uint2 act_words_tab(float v, float sa, float qp, int nan_e, const uint32_t* lut) {
+  const float c = clamp_nan(v / sa, 0.f, qp);
+  const float r = rintf(c);
+  const int e = (r == r) ? (int)r : nan_e;
+  return *reinterpret_cast<const uint2*>(lut + 2 * e);
+}
+template <int NBA_C>
+__device__ inline void act_lut_build_q(const Geo& g, float sa, bool sgn, uint32_t* lut) {
+  if (threadIdx.x == 0) {
+    uint32_t f[1], b[1];
+    act_words<4, NBA_C>(g, __int_as_float(0x7fc00000), sa, sgn, f, b);
+    const int e = (int)g.lsq_qp + 1;
+    lut[2 * e] = f[0];
+    lut[2 * e + 1] = b[0];
+  }
+  act_lut_build<4, NBA_C>(g, sa, sgn, lut);  // entries 0 .. Qp, then the block barrier
+}
+__device__ inline void stage_rows_q(const Geo& g, int WP, int RHx, const float* __restrict__ x, float sa,
+                                    const uint32_t* lut, int b, int ih_first, uint8_t* patch,
+                                    uint8_t* __restrict__ xcb, int own_lo, int own_hi) {
+  const int nan_e = (int)g.lsq_qp + 1;
+  const int QW = g.W >> 2;  // 4-element items per row (W % 4 == 0)
+  const int nrow = g.C * RHx;
+  const int n = nrow * QW;
+  const bool pq = (QW & (QW - 1)) == 0;
+  const int lq = 31 - __builtin_clz(QW);
+  const float invQ = 1.f / (float)QW, invR = 1.f / (float)RHx;
+  const size_t img = (size_t)b * g.C * g.H;
+  for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
+    float4 v[4];
+    int d[4], ihs[4], cs[4], qs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = base + u * (int)blockDim.x;
+      d[u] = -1;
+      if (idx < n) {
+        const int row = pq ? (idx >> lq) : fdiv(idx, QW, invQ), q = pq ? (idx & (QW - 1)) : idx - row * QW;
+        const int c = fdiv(row, RHx, invR);
+        const int ih = ih_first + (row - c * RHx);
+        d[u] = row * WP * 4 + g.PW * 4 + q * 16;
+        ihs[u] = ih;
+        cs[u] = c;
+        qs[u] = q;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)ih < (unsigned)g.H)
+          v[u] = reinterpret_cast<const float4*>(x)[((img + (size_t)c * g.H + ih) * g.W >> 2) + q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (d[u] < 0) continue;
+      uint32_t* p = reinterpret_cast<uint32_t*>(patch + d[u]);
+      if ((unsigned)ihs[u] >= (unsigned)g.H) {
+        p[0] = p[1] = p[2] = p[3] = 0u;
+        continue;
+      }
+      const uint2 w0 = act_words_tab(v[u].x, sa, g.lsq_qp, nan_e, lut);
+      const uint2 w1 = act_words_tab(v[u].y, sa, g.lsq_qp, nan_e, lut);
+      const uint2 w2 = act_words_tab(v[u].z, sa, g.lsq_qp, nan_e, lut);
+      const uint2 w3 = act_words_tab(v[u].w, sa, g.lsq_qp, nan_e, lut);
+      p[0] = w0.x; p[1] = w1.x; p[2] = w2.x; p[3] = w3.x;
+      if (ihs[u] >= own_lo && ihs[u] < own_hi)
+        reinterpret_cast<uint4*>(xcb)[((img + (size_t)cs[u] * g.H + ihs[u]) * g.W >> 2) + qs[u]] =
+            make_uint4(w0.y, w1.y, w2.y, w3.y);
+    }
+  }
+}
+
 // ptab[t] (t < KS*64) for tile i: patch word offset of contraction row f = i*xbar + t relative
 // to a pixel's window origin; 0 for t outside the tile (the weight operand is zero there).
 __device__ inline void build_ptab(const Geo& g, int i, int KSx, int RHx, int WP, int* ptab, int c0 = 0) {
@@ -266,8 +341,10 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                                                          const v4i* __restrict__ wfrag, Params pp,
                                                          const float* __restrict__ sw_p,
                                                          const float* __restrict__ sa_p, float* __restrict__ out,
-                                                         uint8_t* __restrict__ st) {
+                                                         uint8_t* __restrict__ st, const float* __restrict__ xin,
+                                                         const float* __restrict__ sgn_p, uint8_t* __restrict__ xcb) {
   // CSTA 9: the w8a8 fast path of CST 8 without the state words (cimq_c1.hip recomputes them)
+  // xin (module path, NBP 4): the activation quantiser fused into the row staging (stage_rows_q)
   constexpr int CST = CSTA == 9 ? 8 : CSTA;
   constexpr bool WST = CSTA != 9;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -283,6 +360,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   int4* prm = reinterpret_cast<int4*>(cur); cur += (size_t)TT * nkj * NOB * 16 * 16;    // [tt][j][k][NOB*16]
   float* cfl = reinterpret_cast<float*>(cur); cur += (size_t)TT * nkj * NOB * 16 * 4;   // coef, same order
   float* ckl = reinterpret_cast<float*>(cur);
+  // the quantiser's word table [Qp + 1][fwd, bwd] after ckl (launch_fwd_v3 sizes it in)
+  uint32_t* alut = reinterpret_cast<uint32_t*>(cur + al16((size_t)3 * g.nbw * g.nba * 4));
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -326,13 +405,55 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     }
   };
 
+  // every tile's weight side at once (fwd_res): one batched pass per array over all tiles, so its
+  // loads are in flight together (tile by tile it took T x 3 dependent round trips: 8-9 us of a
+  // 40-45 us launch on the 16x16 / 8x8 layers)
+  auto stage_all = [&]() {
+    const int nw = g.nbw * NOB * KS * 64, np = nkj * NOB * 16;
+    const float inv_nw = 1.f / (float)nw, inv_np = 1.f / (float)np;
+    batched_copy<8>(g.T * nw, wfl, [&](int t) -> v4i {
+      const int i = fdiv(t, nw, inv_nw), idx = t - i * nw;
+      const int l = idx & 63, fr = idx >> 6;
+      const int ks = KS == 1 ? 0 : (fr & 1), kob = KS == 1 ? fr : (fr >> 1);
+      const int k = kob >> lnob, ob = kob - (k << lnob);
+      v4i w = {0, 0, 0, 0};
+      if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
+      return w;
+    });
+    if (!flag_lit) {
+      batched_copy<8>(g.T * np, prm, [&](int t) -> int4 {
+        const int i = fdiv(t, np, inv_np), idx = t - i * np;
+        const int col = idx & ((16 << lnob) - 1), jk = idx >> (4 + lnob);
+        const int j = fdiv(jk, g.nbw, inv_nbw), k = jk - j * g.nbw;
+        const int o = og * OBM * 16 + col;
+        int4 p = make_int4(0, 0, 0, 0);
+        if (o < g.Opad) {
+          const int pi = pidx(g, i, j, k, o);
+          p = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
+        }
+        return p;
+      });
+      batched_copy<8>(g.T * np, cfl, [&](int t) -> float {
+        const int i = fdiv(t, np, inv_np), idx = t - i * np;
+        const int col = idx & ((16 << lnob) - 1), jk = idx >> (4 + lnob);
+        const int j = fdiv(jk, g.nbw, inv_nbw), k = jk - j * g.nbw;
+        const int o = og * OBM * 16 + col;
+        return (o < g.Opad) ? pp.coef[pidx(g, i, j, k, o)] : 0.f;
+      });
+    }
+  };
+
   for (int i = 0; i < g.T; ++i) build_ptab(g, i, KS, v.RH, v.WP, ptab + i * KS * 64);
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
   if (v.fwd_res)
 #ifndef CIMQ_EXP_FWD_NOSTAGEW  // attribution builds only (tools/kernel_experiment.py)
-    for (int i = 0; i < g.T; ++i) stage_tile(i, i);
+    stage_all();
 #endif
   zero_lds(reinterpret_cast<uint32_t*>(patch), g.C * v.RH * v.WP * NBP / 4);
+  const bool actq = NBP == 4 && xin != nullptr;  // uniform
+  const float sa_q = actq ? *sa_p : 0.f;
+  const bool sgn_q = actq && *sgn_p != 0.f;
+  if (actq) act_lut_build_q<(CST == 2 || CST == 3) ? CST : 0>(g, sa_q, sgn_q, alut);  // syncs the block
 
   __syncthreads();
   // w8a8: is binary_mask the standard int8-wrapped one (zero exactly where j + k >= 8)?
@@ -348,7 +469,16 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     const int oh0 = p0 >> v.lw;
     __syncthreads();
 #ifndef CIMQ_EXP_FWD_NOSTAGEX
-    stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
+    if (actq) {
+      // input rows this m-tile owns (written once to xcb): its output rows' stride-spans, to the
+      // image's end for its last m-tile; one o-group's blocks write them
+      const int own_lo = blockIdx.y == 0 ? oh0 * g.SH : 0;
+      const int own_hi = blockIdx.y == 0 ? (p0 + 64 == g.P ? g.H : (oh0 + (64 >> v.lw)) * g.SH) : 0;
+      if constexpr (NBP == 4)
+        stage_rows_q(g, v.WP, v.RH, xin, sa_q, alut, b, oh0 * g.SH - g.PH, patch, xcb, own_lo, own_hi);
+    } else {
+      stage_rows<NBP>(g, v.WP, v.RH, xcf, b, oh0 * g.SH - g.PH, patch);
+    }
 #endif
     __syncthreads();
     float acc[OBM][4];
