@@ -297,6 +297,7 @@ inline Plan3 v3_plan(const Geo& g) {
   const size_t fwd_w1 = (size_t)g.nbw * nof * g.KS * 1024 + (size_t)nkj * nof * 16 * (16 + 4);
   const size_t fwd_res = fwd_common + (size_t)g.T * fwd_w1;
   v.fwd_res = fwd_res <= (size_t)tune("FWD_RES_KB", 52) * 1024 ? 1 : 0;
+  v.pf = tune("FWD_PF", 1);
   p.lds_fwd = v.fwd_res ? fwd_res : fwd_common + fwd_w1;
   const size_t lim = kLdsMax - 512;
   p.ok = p.lds_fwd <= lim;

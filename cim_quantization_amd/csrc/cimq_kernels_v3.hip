@@ -35,6 +35,7 @@ struct V3 {
   int NCBT;        // grad_x: max 16-channel blocks one tile touches
   int CB;          // grad_x: 16-channel blocks of the output tile grid (ceil(C/16))
   int NT;          // grad_x: max output tiles (16 positions x 16 channels) per band
+  int pf;          // forward, non-resident tiles: the next tile's weight side prefetched in registers
 };
 
 // floor(n / d) for 0 <= n < 2^22 (inv = 1.f / d): float estimate + one correction step
@@ -375,15 +376,8 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
   // by nbw: integer division is ~30 VALU each, and this prologue runs once per block
   const int lnob = NOB == 4 ? 2 : NOB - 1;
   const float inv_nbw = 1.f / (float)g.nbw;
-  auto stage_tile = [&](int i, int tt) {
-    batched_copy<4>(g.nbw * NOB * KS * 64, wfl + (size_t)tt * g.nbw * NOB * KS * 64, [&](int idx) -> v4i {
-      const int l = idx & 63, fr = idx >> 6;
-      const int ks = KS == 1 ? 0 : (fr & 1), kob = KS == 1 ? fr : (fr >> 1);
-      const int k = kob >> lnob, ob = kob - (k << lnob);
-      v4i w = {0, 0, 0, 0};
-      if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
-      return w;
-    });
+  // the ADC thresholds and coefficients of tile i (the weight side's small part)
+  auto stage_prm = [&](int i, int tt) {
     if (!flag_lit) {
       batched_copy<2>(nkj * NOB * 16, prm + (size_t)tt * nkj * NOB * 16, [&](int idx) -> int4 {
         const int col = idx & ((16 << lnob) - 1), jk = idx >> (4 + lnob);
@@ -403,6 +397,17 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
         return (o < g.Opad) ? pp.coef[pidx(g, i, j, k, o)] : 0.f;
       });
     }
+  };
+  auto stage_tile = [&](int i, int tt) {
+    batched_copy<4>(g.nbw * NOB * KS * 64, wfl + (size_t)tt * g.nbw * NOB * KS * 64, [&](int idx) -> v4i {
+      const int l = idx & 63, fr = idx >> 6;
+      const int ks = KS == 1 ? 0 : (fr & 1), kob = KS == 1 ? fr : (fr >> 1);
+      const int k = kob >> lnob, ob = kob - (k << lnob);
+      v4i w = {0, 0, 0, 0};
+      if (ob < nob) w = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
+      return w;
+    });
+    stage_prm(i, tt);
   };
 
   // every tile's weight side at once (fwd_res): one batched pass per array over all tiles, so its
@@ -443,8 +448,38 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
     }
   };
 
+  // non-resident tiles with a compile-time slice count (CST > 0): the next tile's weight fragments
+  // are loaded into registers while the current tile computes and stored after the tile barrier
+  // (the 16x16 / 8x8 layers, whose tiles do not all fit in LDS, spent 8-9 us per launch staging
+  // them tile by tile); the thresholds are still staged at the barrier (in registers too they cost
+  // the 32-channel layers a wave per SIMD)
+  constexpr int PFW = CST > 0 ? (CST * OBM * KS * 64 + 255) / 256 : 1;
+  const bool pfx = CST > 0 && !v.fwd_res && v.pf && blockDim.x == 256;  // uniform
+  v4i pw[PFW];
+  auto load_tile = [&](int i) {
+    const int nw = g.nbw * NOB * KS * 64;
+#pragma unroll
+    for (int u = 0; u < PFW; ++u) {
+      const int idx = threadIdx.x + u * 256;
+      pw[u] = v4i{0, 0, 0, 0};
+      if (idx < nw) {
+        const int l = idx & 63, fr = idx >> 6;
+        const int ks = KS == 1 ? 0 : (fr & 1), kob = KS == 1 ? fr : (fr >> 1);
+        const int k = kob >> lnob, ob = kob - (k << lnob);
+        if (ob < nob) pw[u] = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * OBM + ob) * WAVE + l];
+      }
+    }
+  };
+  auto store_tile = [&]() {
+    const int nw = g.nbw * NOB * KS * 64;
+#pragma unroll
+    for (int u = 0; u < PFW; ++u)
+      if ((int)threadIdx.x + u * 256 < nw) wfl[threadIdx.x + u * 256] = pw[u];
+  };
+
   for (int i = 0; i < g.T; ++i) build_ptab(g, i, KS, v.RH, v.WP, ptab + i * KS * 64);
   for (int t = threadIdx.x; t < 3 * nkj; t += blockDim.x) ckl[t] = pp.ckj[t];
+  if (pfx) load_tile(0);  // in flight through the prologue and the first row staging
   if (v.fwd_res)
 #ifndef CIMQ_EXP_FWD_NOSTAGEW  // attribution builds only (tools/kernel_experiment.py)
     stage_all();
@@ -490,7 +525,14 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       if (!v.fwd_res) {
         __syncthreads();
 #ifndef CIMQ_EXP_FWD_NOSTAGEW
-        stage_tile(i, 0);
+        if (pfx) {
+          // the weight fragments from the registers loaded a tile ago; the ADC thresholds as before
+          store_tile();
+          stage_prm(i, 0);
+          load_tile(i + 1 < g.T ? i + 1 : 0);  // the next tile (tile 0 again for the next m-tile)
+        } else {
+          stage_tile(i, 0);
+        }
 #endif
         __syncthreads();
       }
