@@ -41,7 +41,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md); the backward
 PEAK_I8_TOPS = 5000.0      # dense int8 MFMA: the forward's bit-sliced partial sums
 PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD-32 x 2.4 GHz (a wave64 VALU op issues over 2 cycles)
 # grad_w + the parameter-gradient epilogue on a second stream (CIMQ_BENCH_OVERLAP=0: one stream,
-# the epilogues chained into the next layer's grad_x launch)
+# the epilogues of all layers packed into a few launches at the end of the backward)
 OVERLAP = os.environ.get("CIMQ_BENCH_OVERLAP", "0") == "1"
 TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r04_final", "pmc_traffic.json"))
 # the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
@@ -106,8 +106,8 @@ class Trainer:
 
     def compute(self, xs, gs):
         """fwd + bwd of every layer; gradients accumulate into the flat bucket.  Each layer's
-        parameter-gradient epilogue rides in the next layer's backward kernels (the chained module
-        backward, functional.chained_epilogues); the last one is flushed at the scope's end."""
+        parameter-gradient epilogue is held back (the chained module backward,
+        functional.chained_epilogues) and all 19 run packed at the scope's end."""
         from cim_quantization_amd.functional import chained_epilogues, prepare_weights
         # the weight side of all 19 prologues in one launch, ahead of the forwards
         prepare_weights(self.layers)

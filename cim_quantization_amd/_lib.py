@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "cimq_module_backward_params",
     "cimq_module_backward_chain",
     "cimq_pending_flush",
+    "cimq_pending_jobs",
     "cimq_module_prepare",
     "cimq_module_shift_supported",
     "cimq_module_shift_forward",
@@ -116,7 +117,7 @@ class QConvDesc(ctypes.Structure):
 class Pending(ctypes.Structure):
     """Mirror of ``cimq_pending`` (opaque; zero-initialised by ctypes)."""
 
-    _fields_ = [("opaque", ctypes.c_uint64 * 128)]
+    _fields_ = [("opaque", ctypes.c_uint64 * 2048)]
 
 
 class Sizes(ctypes.Structure):
@@ -167,6 +168,8 @@ def _bind(lib):
                                                [ctypes.POINTER(Pending), _VP])
     lib.cimq_pending_flush.restype = ctypes.c_int
     lib.cimq_pending_flush.argtypes = [ctypes.POINTER(Pending), _VP]
+    lib.cimq_pending_jobs.restype = ctypes.c_int
+    lib.cimq_pending_jobs.argtypes = [ctypes.POINTER(Pending)]
     lib.cimq_module_prepare.restype = ctypes.c_int
     lib.cimq_module_prepare.argtypes = [ctypes.c_int, ctypes.POINTER(PrepareItem), _VP]
     lib.cimq_module_shift_supported.restype = ctypes.c_int

@@ -58,14 +58,6 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
   return CIMQ_OK;
 }
 
-static Carry no_carry() {
-  Carry c;
-  memset(&c, 0, sizeof(c));
-  return c;
-}
-
-// carry: a previous layer's finish to run inside the v7 grad_x launch (struct Carry); only the v7
-// path can carry, so callers check v7_plan(g).ok before passing a non-empty one
 // layers whose backward is the separate v7 grad_x / grad_w pair: with CIMQ_LSQ_DEFER_GW the grad_w
 // kernel leaves cimq_module_backward for cimq_module_backward_params (the fused / first-conv kernels
 // and the general paths produce both in one pass)
@@ -77,10 +69,9 @@ static bool gw_deferrable(const Geo& g) {
 // kernel of a gw_deferrable layer
 int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const float* sa, const float* signed_act,
                      const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool* lsq_fused,
-                     const Carry& carry = no_carry(), int parts = 3) {
+                     int parts = 3) {
   if (parts == 2 && !gw_deferrable(g)) return fail(CIMQ_EINVAL, "internal: grad_w alone on a single-pass backward");
   if (!v7_bwd(g)) {
-    if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
     if (dense_plan(g)) {
       *lsq_fused = g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0;
       return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s, *lsq_fused ? x : nullptr, sa);
@@ -91,23 +82,22 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
   if (pc.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
-    return launch_c1(g, pc, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    return launch_c1(g, pc, ctx, sw, sa, gout, x, gx, ws, s, lsq);
   }
   const Plan9 p9 = v9_plan(g);
   if (p9.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
-    return launch_fused(g, p9, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry);
+    return launch_fused(g, p9, ctx, sw, sa, gout, x, gx, ws, s, lsq);
   }
   const Plan7 p7 = v7_plan(g);
   if (p7.ok) {
     const bool lsq = g.input_kind == CIMQ_INPUT_RAW_LSQ;
     *lsq_fused = lsq;
-    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
-    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
-    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    if (g.NBP == 8) return launch_v7_n<8, 8>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
+    if (g.nbw == 2) return launch_v7_n<2, 2>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
+    return launch_v7_n<3, 3>(g, p7, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
   }
-  if (carry.finish) return fail(CIMQ_EINVAL, "internal: carried epilogue on a non-v7 backward");
   if (dense_plan(g)) {
     *lsq_fused = g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0;
     return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s, *lsq_fused ? x : nullptr, sa);
@@ -343,14 +333,23 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
   return CIMQ_OK;
 }
 
-// the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes
-static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
+// the module backward's epilogue: grad_w + weight-LSQ backward, grad_alpha_cim, the step sizes;
+// tail_blocks is the grid of its slab-sum launch
+struct TailLaunch {
+  int tail_blocks;
+  Geo g;
+  LsqArgs q;
+  ModuleTail a;
+};
+
+static TailLaunch tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
                       float* grad_alpha_weight, float* grad_alpha_cim, int gaq_ready = 0) {
   const bool has_alpha = la.nbits_alpha > 0;
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
-  Carry j = no_carry();
+  TailLaunch j;
+  memset(&j, 0, sizeof(j));
   ModuleTail& a = j.a;
   a.gw_slab = reinterpret_cast<const float*>(w + W.gw_slab);
   a.ga_slab = reinterpret_cast<const float*>(w + W.ga_slab);
@@ -364,15 +363,18 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   a.grad_alpha_act = grad_alpha_act;
   a.grad_alpha_w = grad_alpha_weight;
   a.grad_alpha_cim = grad_alpha_cim;
-  a.pp = params_of(g, const_cast<uint8_t*>(c));
+  a.ckj = params_of(g, const_cast<uint8_t*>(c)).ckj;
   a.cgrad = (float)(1.0 / sqrt((double)g.B * g.T * g.nbw * g.nba * g.P * g.O * (double)g.qp));  // lsq.py:323,330
   a.nchunks = W.nchunks_bwd;
   // few chunks and many outputs (the dense path's 8 chunks of a 1024 x 1024 layer): one output per
   // thread (16 k blocks of 64 outputs each took 67 us for 34 MB of slab)
   const long long nout_w = (long long)g.T * g.FBT * 16 * g.Opad;
   a.wide = (a.nchunks <= 16 && nout_w >= (1 << 18) && tune("WIDE_SLAB", 1)) ? 1 : 0;
-  a.nwb = cdiv(nout_w, a.wide ? 1024 : 64);
-  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, a.wide ? 1024 : 64) : 0;
+  // otherwise float4 reads, 16-lane rows when the chunks are many (reduce_chunks4)
+  a.lpr = a.nchunks > tune("TAIL_LPR_CHUNKS", 64) ? 16 : 64;
+  const int per_blk = a.wide ? 1024 : 4 * a.lpr;
+  a.nwb = cdiv(nout_w, per_blk);
+  a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, per_blk) : 0;
   a.napart = act_parts(g);
   a.accum = (q->flags & CIMQ_LSQ_ACCUMULATE_GRADS) ? 1 : 0;
   a.gapart = (has_alpha && la.nalpha > kFinishInReg && tune("WIDE_TAIL", 1)) ? reinterpret_cast<float*>(w + W.gapart) : nullptr;
@@ -380,16 +382,15 @@ static Carry tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, c
   j.g = g;
   j.q = la;
   j.tail_blocks = a.nwb + a.nga;
-  j.finish = 1;
   return j;
 }
 
-static int launch_tail(const Carry& j, hipStream_t s) {
+static int launch_tail(const TailLaunch& j, hipStream_t s) {
   hipLaunchKernelGGL(module_bwd_tail_kernel, dim3(j.tail_blocks), dim3(1024), 0, s, j.g, j.q, j.a);
   return check_hip("module_bwd_tail");
 }
 
-static int launch_finish(const Carry& j, hipStream_t s) {
+static int launch_finish(const TailLaunch& j, hipStream_t s) {
   if (j.a.gapart)
     hipLaunchKernelGGL(module_bwd_finish_wide_kernel, dim3(cdiv(j.q.nalpha, 1024)), dim3(1024), 0, s, j.q, j.a);
   else
@@ -400,21 +401,81 @@ static int launch_finish(const Carry& j, hipStream_t s) {
 static int module_tail(Geo g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
                        const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
                        float* grad_alpha_weight, float* grad_alpha_cim, hipStream_t s, int gaq_ready = 0) {
-  const Carry j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+  const TailLaunch j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
                            grad_alpha_cim, gaq_ready);
   CIMQ_TRY(launch_tail(j, s));
   return launch_finish(j, s);
 }
 
-// cimq_pending (caller-owned host memory): the epilogue a chained module backward left behind,
-// and which part of it has run
+// cimq_pending (caller-owned host memory): the epilogues chained module backwards left behind,
+// in call order, with each one's tail grid
+constexpr int kPendingJobs = 32;
 struct Pending {
   uint32_t magic;
-  int tail_done;
-  Carry job;
+  int n;
+  int nblk[kPendingJobs];
+  TailJob job[kPendingJobs];
 };
 static_assert(sizeof(Pending) <= sizeof(cimq_pending), "cimq_pending too small");
 constexpr uint32_t kPendingMagic = 0x63696d70u;
+
+static TailJob tail_job_of(const TailLaunch& c) {
+  TailJob t;
+  t.t = TailGeo{c.g.T, c.g.FBT, c.g.Opad, c.g.O, c.g.xbar, c.g.K, c.g.nbw, c.g.nba};
+  t.q = c.q;
+  t.a = c.a;
+  return t;
+}
+
+// every pending tail (packs of kTailJobs per launch), then every finish: the launch boundary
+// orders each finish after its tail's partials
+static int pending_run(Pending* pd, hipStream_t s) {
+  if (pd->magic != kPendingMagic) return CIMQ_OK;
+  const int n = pd->n;
+  pd->magic = 0;
+  pd->n = 0;
+  for (int i = 0; i < n;) {
+    TailPack tp;
+    tp.n = 0;
+    int blk = 0;
+    for (; i < n && tp.n < kTailJobs; ++i, ++tp.n) {
+      tp.blk0[tp.n] = blk;
+      tp.job[tp.n] = pd->job[i];
+      blk += pd->nblk[i];
+    }
+    tp.blk0[tp.n] = blk;
+    hipLaunchKernelGGL(module_tail_many_kernel, dim3(blk), dim3(1024), 0, s, tp);
+    CIMQ_TRY(check_hip("module_tail_many"));
+  }
+  for (int i = 0; i < n;) {
+    FinishPack fp;
+    fp.n = 0;
+    int blk = 0;
+    for (; i < n && fp.n < kFinishJobs; ++i, ++fp.n) {
+      const TailJob& t = pd->job[i];
+      fp.blk0[fp.n] = blk;
+      fp.job[fp.n].q = t.q;
+      fp.job[fp.n].a = t.a;
+      blk += t.a.gapart ? cdiv(t.q.nalpha, 1024) : 1;
+    }
+    fp.blk0[fp.n] = blk;
+    hipLaunchKernelGGL(module_finish_many_kernel, dim3(blk), dim3(1024), 0, s, fp);
+    CIMQ_TRY(check_hip("module_finish_many"));
+  }
+  return CIMQ_OK;
+}
+
+// a pending epilogue writing any gradient buffer this one writes (a layer run twice in one
+// backward): the two must not share a launch
+static bool pending_overlaps(const Pending* pd, const ModuleTail& a) {
+  for (int i = 0; i < pd->n; ++i) {
+    const ModuleTail& b = pd->job[i].a;
+    if (b.grad_weight == a.grad_weight || b.grad_alpha_act == a.grad_alpha_act || b.grad_alpha_w == a.grad_alpha_w ||
+        (a.grad_alpha_cim && b.grad_alpha_cim == a.grad_alpha_cim))
+      return true;
+  }
+  return false;
+}
 
 static int lsq_args(const Geo& g, const cimq_lsq_desc* q, LsqArgs* a) {
   if (!q) return fail(CIMQ_EINVAL, "null LSQ descriptor");
@@ -567,14 +628,6 @@ int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, c
                              out, ctx, ws, stream);
 }
 
-static int pending_run(Pending* pd, hipStream_t s) {
-  if (pd->magic != kPendingMagic) return CIMQ_OK;
-  if (!pd->tail_done) CIMQ_TRY(launch_tail(pd->job, s));
-  CIMQ_TRY(launch_finish(pd->job, s));
-  pd->magic = 0;
-  return CIMQ_OK;
-}
-
 static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
                                 const float* x, const float* weight, const float* alpha_act,
                                 const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
@@ -611,20 +664,9 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
     CIMQ_TRY(check_hip("nchw_to_bpo"));
     gsrc = bpo;
   }
-  // chained: the previous layer's finish rides in this layer's v7 grad_x launch (block 0); other
-  // paths run it first on its own
-  Carry carry = no_carry();
-  if (pend && pend->magic == kPendingMagic) {
-    if (v7_plan(g).ok && pend->tail_done) {
-      carry = pend->job;
-      pend->magic = 0;
-    } else {
-      CIMQ_TRY(pending_run(pend, s));
-    }
-  }
   bool lsq_fused = false;
   const bool defer = (q->flags & CIMQ_LSQ_DEFER_GW) && gw_deferrable(g);
-  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused, carry, defer ? 1 : 3));
+  CIMQ_TRY(dispatch_bwd_any(g, c, sw, sa, signed_act, gsrc, x, grad_x, w, s, &lsq_fused, defer ? 1 : 3));
   // the act-LSQ partials: fused into the fast grad_x kernel, a separate pass otherwise
   float* part = reinterpret_cast<float*>(w + W.lsq_part);
   int nparts;
@@ -639,13 +681,16 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   }
   if (nparts != act_parts(g)) return fail(CIMQ_EINVAL, "internal: act-LSQ partial count mismatch");
   if (pend) {
-    // the slab reductions run now (as extra 256-thread blocks of the next layer's grad_x they
-    // measured slower: each takes 4x the serial loads of a 1024-thread tail block); the
-    // one-block finish waits for the next chained call's grad_x or cimq_pending_flush
-    pend->job = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
-                         grad_alpha_cim);
-    CIMQ_TRY(launch_tail(pend->job, s));
-    pend->tail_done = 1;
+    // the epilogue joins the pending ones: cimq_pending_flush (or a full list, or a layer whose
+    // gradient buffers a pending one writes) launches them all, packed
+    const TailLaunch j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
+                             grad_alpha_cim);
+    if (pend->magic == kPendingMagic && (pend->n == kPendingJobs || pending_overlaps(pend, j.a)))
+      CIMQ_TRY(pending_run(pend, s));
+    if (pend->magic != kPendingMagic) pend->n = 0;
+    pend->nblk[pend->n] = j.tail_blocks;
+    pend->job[pend->n] = tail_job_of(j);
+    ++pend->n;
     pend->magic = kPendingMagic;
     return CIMQ_OK;
   }
@@ -679,6 +724,11 @@ int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
   return module_backward_impl(d, q, grad_out, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act,
                               ctx, grad_x, grad_weight, grad_alpha_act, grad_alpha_weight, grad_alpha_cim, ws, pd,
                               stream);
+}
+
+int cimq_pending_jobs(const cimq_pending* pending) {
+  const Pending* pd = reinterpret_cast<const Pending*>(pending);
+  return (pd && pd->magic == kPendingMagic) ? pd->n : 0;
 }
 
 int cimq_pending_flush(cimq_pending* pending, void* stream) {
@@ -727,8 +777,7 @@ int cimq_module_backward_params(const cimq_conv_desc* d, const cimq_lsq_desc* q,
     g.onchw = 1;
     const float* scal = reinterpret_cast<const float*>(wreg(g, c) + ctx_layout(g).lsq_scal);
     bool lsq_fused = false;
-    CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, nullptr, grad_out, nullptr, nullptr, w, s, &lsq_fused,
-                              no_carry(), 2));
+    CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, nullptr, grad_out, nullptr, nullptr, w, s, &lsq_fused, 2));
   }
   return module_tail(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
                      grad_alpha_cim, s);

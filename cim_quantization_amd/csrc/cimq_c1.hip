@@ -43,15 +43,11 @@ __global__ __launch_bounds__(512) void cim_bwd_c1_kernel(Geo g, VC1 v, const uin
                                                          const float* __restrict__ sa_p, const float* __restrict__ gout,
                                                          const float* __restrict__ x, float* __restrict__ gx,
                                                          float* __restrict__ gw_slab, float* __restrict__ ga_slab,
-                                                         float* __restrict__ gsa_part, Carry cr) {
+                                                         float* __restrict__ gsa_part) {
   constexpr int NB = 8, NKJ = 64, NKS = 4;  // w8a8, one 16-channel block: kappa = (k, o) = 128 = 4 K-steps
   constexpr int GP = 132;                   // grad_out LDS row pitch (128 pixels + 4)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (cr.finish && blockIdx.x == 0) {
-    module_finish_block(cr.q, cr.a, reinterpret_cast<float*>(smem));
-    return;
-  }
-  const int b = (int)blockIdx.x - (cr.finish ? 1 : 0);
+  const int b = (int)blockIdx.x;
   uint8_t* xp = smem + v.o_xp;   // forward slice words of the step's rows [C][RH][WP] x 8 B
   uint8_t* hp = smem + v.o_hp;   // backward (int8 ctx) slice words, same layout
   int* ptab = reinterpret_cast<int*>(smem + v.o_ptab);   // [64] word offset of row f in a window

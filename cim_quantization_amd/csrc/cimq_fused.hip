@@ -55,7 +55,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
                                                             const uint32_t* __restrict__ xcb,
                                                             const float* __restrict__ x, float* __restrict__ gx,
                                                             float* __restrict__ gw_slab, float* __restrict__ ga_slab,
-                                                            float* __restrict__ gsa_part, Carry cr) {
+                                                            float* __restrict__ gsa_part) {
   constexpr int NKJ = NB * NB;
   constexpr int NKS = (NB * OBX + 1) / 2;
   constexpr int WPO = 4 / OBX;  // grad_w waves per 16-channel output block
@@ -68,12 +68,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
   constexpr int PST = (16 * O + 511) / 512;  // 16-B pieces of a unit's state words / grad_out per thread
   constexpr int GP = 68;        // grad_out LDS row pitch (floats): 16-B reads of 16 channels hit distinct banks
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // the previous layer's finish (struct Carry) in block 0, as cim_bwd_gx_v8_kernel
-  if (cr.finish && blockIdx.x == 0) {
-    module_finish_block(cr.q, cr.a, reinterpret_cast<float*>(smem));
-    return;
-  }
-  const int b = (int)blockIdx.x - (cr.finish ? 1 : 0);
+  const int b = (int)blockIdx.x;
   float* ring = reinterpret_cast<float*>(smem + v.o_ring);
   float* cel = reinterpret_cast<float*>(smem + v.o_cel);  // [0, NKJ): cE (grad_x); [NKJ, 2 NKJ): cD (grad_w)
   float* red = reinterpret_cast<float*>(smem + v.o_red);

@@ -861,16 +861,16 @@ int launch_alpha_init_sums(const Geo& g, const uint8_t* ctx, const float* sw, co
 template <int NBW, int NBA>
 int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
-                const Carry& carry, int parts);
+                int parts);
 #define CIMQ_V7_SIG(NBW, NBA)                                                                              \
   int launch_v7_n<NBW, NBA>(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa, \
                             const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, \
-                            const Carry& carry, int parts)
+                            int parts)
 // cimq_part_fused.hip: the fused backward (v9_plan)
 int launch_fused(const Geo& g, const Plan9& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
-                 const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry);
+                 const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq);
 int launch_c1(const Geo& g, const PlanC1& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
-              const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq, const Carry& carry);
+              const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq);
 extern template CIMQ_V7_SIG(2, 2);
 extern template CIMQ_V7_SIG(3, 3);
 extern template CIMQ_V7_SIG(8, 8);

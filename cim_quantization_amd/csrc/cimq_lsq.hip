@@ -184,8 +184,8 @@ __global__ __launch_bounds__(256) void prep_weights_many_kernel(PrepPack p) {
                       reinterpret_cast<float*>(red4));
 }
 
-__global__ __launch_bounds__(1024) void module_bwd_tail_kernel(Geo g, LsqArgs q, ModuleTail a) {
-  __shared__ float red[1024];
+__global__ __launch_bounds__(1024, 8) void module_bwd_tail_kernel(Geo g, LsqArgs q, ModuleTail a) {
+  __shared__ __attribute__((aligned(16))) float red[4 * 1024];
   const int b = (int)blockIdx.x;
   if (b < a.nwb) gw_lsq_role(g, q, a, b, red);
   else galpha_role(g, q, a, b - a.nwb, red);
@@ -202,7 +202,73 @@ __global__ __launch_bounds__(1024) void module_bwd_finish_kernel(LsqArgs q, Modu
 
 __global__ __launch_bounds__(1024) void module_bwd_finish_wide_kernel(LsqArgs q, ModuleTail a) {
   __shared__ __attribute__((aligned(16))) float red[16 * 8];
-  module_finish_wide_block(q, a, red);
+  module_finish_wide_block(q, a, red, (int)blockIdx.x);
+}
+
+// The epilogues of several chained layers in two launches (cimq_pending_flush): a layer's tail is
+// a few microseconds of slab sums, mostly launch ramp and drain at the small layers, so the
+// chained backward packs every layer's tail blocks into one grid and every finish into another.
+// The jobs travel as kernel arguments, with only the geometry fields the two roles read.
+struct TailGeo {
+  int T, FBT, Opad, O, xbar, K, nbw, nba;
+};
+struct TailJob {
+  TailGeo t;
+  LsqArgs q;
+  ModuleTail a;
+};
+constexpr int kTailJobs = 20;
+struct TailPack {
+  int n;
+  int blk0[kTailJobs + 1];  // first block of each job, blk0[n] = grid
+  TailJob job[kTailJobs];
+};
+static_assert(sizeof(TailPack) <= 4000, "TailPack exceeds the kernel-argument budget");
+
+__device__ inline Geo geo_of(const TailGeo& t) {
+  Geo g{};
+  g.T = t.T;
+  g.FBT = t.FBT;
+  g.Opad = t.Opad;
+  g.O = t.O;
+  g.xbar = t.xbar;
+  g.K = t.K;
+  g.nbw = t.nbw;
+  g.nba = t.nba;
+  return g;
+}
+
+__global__ __launch_bounds__(1024, 8) void module_tail_many_kernel(TailPack p) {
+  __shared__ __attribute__((aligned(16))) float red[4 * 1024];
+  int j = 0;
+  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  const TailJob& jb = p.job[j];
+  const Geo g = geo_of(jb.t);
+  const int b = (int)blockIdx.x - p.blk0[j];
+  if (b < jb.a.nwb) gw_lsq_role(g, jb.q, jb.a, b, red);
+  else galpha_role(g, jb.q, jb.a, b - jb.a.nwb, red);
+}
+
+struct FinishJob {
+  LsqArgs q;
+  ModuleTail a;
+};
+constexpr int kFinishJobs = 24;
+struct FinishPack {
+  int n;
+  int blk0[kFinishJobs + 1];
+  FinishJob job[kFinishJobs];
+};
+static_assert(sizeof(FinishPack) <= 4000, "FinishPack exceeds the kernel-argument budget");
+
+// one block per job, cdiv(nalpha, 1024) for a wide alpha_cim (module_finish_wide_block)
+__global__ __launch_bounds__(1024) void module_finish_many_kernel(FinishPack p) {
+  __shared__ __attribute__((aligned(16))) float red[16 * 8];
+  int j = 0;
+  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  const FinishJob& jb = p.job[j];
+  if (jb.a.gapart) module_finish_wide_block(jb.q, jb.a, red, (int)blockIdx.x - p.blk0[j]);
+  else module_finish_block(jb.q, jb.a, red);
 }
 
 // max / min of a wide alpha_cim (> kFinishInReg elements) per block, for the prologue's weight

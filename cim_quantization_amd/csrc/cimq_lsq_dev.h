@@ -1,6 +1,5 @@
-// cimq_lsq_dev.h -- device side of the LSQ quantiser backward shared by the module epilogue
-// kernels (cimq_lsq.hip) and by the v7 backward kernels (cimq_v7.hip), which can run a previous
-// layer's epilogue in extra workgroups (the chained module backward, cimq_module_backward_chain).
+// cimq_lsq_dev.h -- device side of the LSQ quantiser backward: the module epilogue kernels
+// (cimq_lsq.hip), one layer per launch or packed over a chain of layers (cimq_pending_flush).
 #pragma once
 #include "cimq_kernels_v3.hip"
 
@@ -83,13 +82,16 @@ struct ModuleTail {
   float* grad_alpha_act;
   float* grad_alpha_w;
   float* grad_alpha_cim;
-  Params pp;
-  float* gapart;  // wide alpha_cim (> kFinishInReg elements): [nga][4] first-sweep partials, else null
-  float cgrad;    // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
-  int nchunks, nwb, nga, napart, accum;
-  int gaq_ready;  // d loss / d alpha_q already in gaq (the shift ADC's statistics kernel): no slab sums
-  int wide;       // few chunks, many outputs (the dense path): one output per thread of a 1024-thread
-                  // block (nwb / nga count such blocks), the chunks summed in order by that thread
+  const float* ckj;  // Params::ckj of the layer
+  float* gapart;     // wide alpha_cim (> kFinishInReg elements): [nga][4] first-sweep partials, else null
+  float cgrad;       // 1 / sqrt(numel(ps) Qp_adc) (lsq.py:323,330)
+  int nchunks, nwb, nga, napart;
+  uint8_t accum;
+  uint8_t gaq_ready;  // d loss / d alpha_q already in gaq (the shift ADC's statistics kernel): no slab sums
+  uint8_t wide;       // few chunks, many outputs (the dense path): one output per thread of a 1024-thread
+                      // block (nwb / nga count such blocks), the chunks summed in order by that thread
+  uint8_t lpr;        // not wide: float4 slab reads, lpr lanes (16 or 64) x 4 outputs per block and
+                      // 1024 / lpr chunk groups (reduce_chunks4); nwb / nga count such blocks
 };
 // alpha_cim sizes the one-block epilogue keeps in registers (module_finish_block); larger ones
 // (the QuantLinear layers: T * nbw * nba * O = 131072 at 1024 -> 1024 w4a4) take the wide path:
@@ -114,45 +116,113 @@ __device__ inline float sum_chunks_serial(const float* __restrict__ slab, size_t
   return v;
 }
 
+// The slab sum of four consecutive outputs per lane: the block's lpr-lane rows (lpr = 16 or 64)
+// each take every nsub-th chunk, then the first row sums the rows in
+// order through LDS.  Many chunks (the per-image slabs of the fused / first-conv kernels, 256-512)
+// take lpr 16: 64 chunk rows, so one batch of loads per lane instead of four.  red: blockDim float4s.
+__device__ inline float4 reduce_chunks4(const float* __restrict__ slab, size_t chunk_stride, int nchunks, size_t idx,
+                                        int lpr, float4* red) {
+  const int sub = (int)threadIdx.x / lpr, nsub = (int)blockDim.x / lpr;
+  // 4 accumulators, 4 float4 loads in flight: the kernel stays within 64 VGPRs (two 1024-thread
+  // blocks per CU)
+  float4 a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int c = sub;
+  for (; c + 3 * nsub < nchunks; c += 4 * nsub) {
+    float4 t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const float4*>(slab + (size_t)(c + u * nsub) * chunk_stride + idx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u].x += t[u].x;
+      a[u].y += t[u].y;
+      a[u].z += t[u].z;
+      a[u].w += t[u].w;
+    }
+  }
+  for (; c < nchunks; c += nsub) {
+    const float4 t = *reinterpret_cast<const float4*>(slab + (size_t)c * chunk_stride + idx);
+    a[0].x += t.x;
+    a[0].y += t.y;
+    a[0].z += t.z;
+    a[0].w += t.w;
+  }
+  float4 r;
+  r.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+  r.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+  r.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+  r.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
+  red[threadIdx.x] = r;
+  __syncthreads();
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sub == 0)
+#pragma unroll 8
+    for (int t = 0; t < nsub; ++t) {
+      const float4 u = red[threadIdx.x + lpr * t];
+      v.x += u.x;
+      v.y += u.y;
+      v.z += u.z;
+      v.w += u.w;
+    }
+  return v;
+}
+
+// one output's weight-quantiser backward (below), in two halves: its loads (gw_pre, issued before
+// the slab sums so their latency overlaps them), then grad_weight and the two d / d sw terms
+struct GwPre {
+  int e;  // weight element (O * K < 2^31), -1: a padding row / channel
+  float w, old;
+};
+
+__device__ inline GwPre gw_pre(const Geo& g, const ModuleTail& a, size_t idx) {
+  GwPre p;
+  const int o = (int)(idx % g.Opad);
+  const size_t row = idx / g.Opad;
+  const int i = (int)(row / (g.FBT * 16)), fl = (int)(row - (size_t)i * g.FBT * 16);
+  const int f = i * g.xbar + fl;
+  const bool ok = o < g.O && fl < g.xbar && f < g.K;
+  p.e = ok ? o * g.K + f : -1;
+  p.w = ok ? a.weight[p.e] : 0.f;
+  p.old = (ok && a.accum) ? a.grad_weight[p.e] : 0.f;
+  return p;
+}
+
+__device__ inline void gw_fin(const LsqArgs& q, const ModuleTail& a, const GwPre& p, float vsum, float nbw,
+                              float& p_mul, float& p_div) {
+  if (p.e < 0) return;
+  const float sa = a.scal[0], sw = a.scal[1];
+  const float G = vsum * (sa / nbw);  // d loss / d w_q (as reduce_gw_v3)
+  const float t1 = p.w / sw;
+  const float c = clamp_nan(t1, q.qn_w, q.qp_w);
+  const float rp = round_pass_value(c);
+  const float grad_rp = G * sw;
+  const bool pass = (t1 >= q.qn_w) && (t1 <= q.qp_w);
+  const float grad_t1 = pass ? grad_rp : 0.f;
+  const float gwv = grad_t1 / sw;
+  a.grad_weight[p.e] = a.accum ? p.old + gwv : gwv;
+  p_mul += G * rp;
+  p_div += -grad_t1 * (t1 / sw);
+}
+
 __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const size_t rows = (size_t)g.T * g.FBT * 16;
   const size_t nout = rows * g.Opad;
-  const size_t idx = a.wide ? (size_t)blk * blockDim.x + threadIdx.x : (size_t)blk * 64 + (threadIdx.x & 63);
-  const int sub = a.wide ? 0 : threadIdx.x >> 6;
-  const float vsum = a.wide ? (idx < nout ? sum_chunks_serial(a.gw_slab, nout, a.nchunks, idx) : 0.f)
-                            : reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  float p_mul = 0.f, p_div = 0.f;
-  if (sub == 0 && idx < nout) {
-    const int o = (int)(idx % g.Opad);
-    const size_t row = idx / g.Opad;
-    const int i = (int)(row / (g.FBT * 16)), fl = (int)(row - (size_t)i * g.FBT * 16);
-    const int f = i * g.xbar + fl;
-    if (o < g.O && fl < g.xbar && f < g.K) {
-      const float sa = a.scal[0], sw = a.scal[1];
-      const float G = vsum * (sa / (float)g.nbw);  // d loss / d w_q (as reduce_gw_v3)
-      const size_t e = (size_t)o * g.K + f;
-      const float t1 = a.weight[e] / sw;
-      const float c = clamp_nan(t1, q.qn_w, q.qp_w);
-      const float rp = round_pass_value(c);
-      const float grad_rp = G * sw;
-      const bool pass = (t1 >= q.qn_w) && (t1 <= q.qp_w);
-      const float grad_t1 = pass ? grad_rp : 0.f;
-      const float gwv = grad_t1 / sw;
-      a.grad_weight[e] = a.accum ? a.grad_weight[e] + gwv : gwv;
-      p_mul = G * rp;
-      p_div = -grad_t1 * (t1 / sw);
-    }
-  }
-  if (a.wide) {  // every thread holds an output: a block reduction
-    const float4 r = block_sum4(make_float4(p_mul, p_div, 0.f, 0.f), red);
-    if (threadIdx.x == 0) {
-      a.wpart[2 * blk] = r.x;
-      a.wpart[2 * blk + 1] = r.y;
-    }
-    return;
-  }
-  // both partials live in the first wave only: a butterfly there, no block barriers
-  if (sub == 0) {
+  if (!a.wide) {  // nout % 16 == 0 (Opad)
+    const size_t i0 = ((size_t)blk * a.lpr + (threadIdx.x & (a.lpr - 1))) * 4;
+    const bool mine = (int)threadIdx.x < a.lpr && i0 < nout;
+    GwPre pre[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pre[u] = mine ? gw_pre(g, a, i0 + u) : GwPre{-1, 0.f, 0.f};
+    const float4 v = reduce_chunks4(a.gw_slab, nout, a.nchunks, i0 < nout ? i0 : 0, a.lpr,
+                                    reinterpret_cast<float4*>(red));
+    if (threadIdx.x >= 64) return;
+    float p_mul = 0.f, p_div = 0.f;
+    const float nbw = (float)g.nbw;
+    gw_fin(q, a, pre[0], v.x, nbw, p_mul, p_div);
+    gw_fin(q, a, pre[1], v.y, nbw, p_mul, p_div);
+    gw_fin(q, a, pre[2], v.z, nbw, p_mul, p_div);
+    gw_fin(q, a, pre[3], v.w, nbw, p_mul, p_div);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       p_mul += __shfl_xor(p_mul, o);
@@ -162,51 +232,101 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
       a.wpart[2 * blk] = p_mul;
       a.wpart[2 * blk + 1] = p_div;
     }
+    return;
+  }
+  // wide: every thread holds an output, a block reduction
+  const size_t idx = (size_t)blk * blockDim.x + threadIdx.x;
+  const float vsum = idx < nout ? sum_chunks_serial(a.gw_slab, nout, a.nchunks, idx) : 0.f;
+  float p_mul = 0.f, p_div = 0.f;
+  if (idx < nout) gw_fin(q, a, gw_pre(g, a, idx), vsum, (float)g.nbw, p_mul, p_div);
+  const float4 r = block_sum4(make_float4(p_mul, p_div, 0.f, 0.f), red);
+  if (threadIdx.x == 0) {
+    a.wpart[2 * blk] = r.x;
+    a.wpart[2 * blk + 1] = r.y;
   }
 }
 
-__device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
+// one output of the grad_alpha slab: G = d loss / d alpha_q into gaq; with gapart set, its terms of
+// alpha_cim_bwd_block's first sweep.  Loads first (ga_pre, ahead of the slab sums), as gw_pre.
+struct GaPre {
+  int e;       // alpha_cim element (i, k, j, o), -1: a padding channel
+  float g, v;  // gaq (gaq_ready), alpha_cim (gapart)
+};
+
+__device__ inline GaPre ga_pre(const Geo& g, const ModuleTail& a, size_t idx) {
+  GaPre p;
   const int nkj = g.nbw * g.nba;
-  const size_t nout = (size_t)g.T * nkj * g.Opad;
-  const size_t idx = a.wide ? (size_t)blk * blockDim.x + threadIdx.x : (size_t)blk * 64 + (threadIdx.x & 63);
-  const float s = a.gaq_ready ? 0.f
-                  : a.wide ? (idx < nout ? sum_chunks_serial(a.ga_slab, nout, a.nchunks, idx) : 0.f)
-                           : reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
-  if (!a.wide && (threadIdx.x >> 6) != 0) return;
+  const int o = (int)(idx % g.Opad);
+  const int qq = (int)(idx / g.Opad);  // (i, k, j)
+  const int kj = qq % nkj, i = qq / nkj;
+  const int k = kj / g.nba, j = kj - k * g.nba;
+  p.e = o < g.O ? ((i * g.nbw + k) * g.nba + j) * g.O + o : -1;
+  p.g = (p.e >= 0 && a.gaq_ready) ? a.gaq[p.e] : 0.f;
+  p.v = (p.e >= 0 && a.gapart) ? a.alpha_cim[p.e] : 0.f;
+  return p;
+}
+
+__device__ inline float4 ga_fin(const Geo& g, const LsqArgs& q, const ModuleTail& a, const GaPre& p, size_t idx,
+                                float s) {
   float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (idx < nout) {
-    const int o = (int)(idx % g.Opad);
-    const size_t qq = idx / g.Opad;  // (i, k, j)
-    if (o < g.O) {
-      const int kj = (int)(qq % nkj);
-      const int i = (int)(qq / nkj);
-      const int k = kj / g.nba, j = kj - k * g.nba;
-      const size_t e = (((size_t)i * g.nbw + k) * g.nba + j) * g.O + o;
-      float G;
-      if (a.gaq_ready) {
-        G = a.gaq[e];
-      } else {
-        G = (a.cgrad * a.pp.ckj[kj]) * s;  // lsq.py:323-334
-        a.gaq[e] = G;
-      }
-      if (a.gapart) {  // alpha_cim_bwd_block's first sweep, this element
-        const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
-        const float qp_al = (float)((1 << q.nbits_alpha) - 1);
-        const float v = a.alpha_cim[e];
-        const float t = v / scale;
-        const float rp = round_pass_value(t);
-        const float c = clamp_nan(rp, 1.f, qp_al);
-        const bool pass = (rp >= 1.f) && (rp <= qp_al);
-        const float gt = pass ? G * scale : 0.f;
-        part = make_float4(G * c, -gt * (t / scale), ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f,
-                           ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f);
-      }
+  if (p.e < 0) return part;
+  float G;
+  if (a.gaq_ready) {
+    G = p.g;
+  } else {
+    const int kj = (int)((idx / g.Opad) % (size_t)(g.nbw * g.nba));
+    G = (a.cgrad * a.ckj[kj]) * s;  // lsq.py:323-334
+    a.gaq[p.e] = G;
+  }
+  if (a.gapart) {  // alpha_cim_bwd_block's first sweep, this element
+    const float scale = a.scal[2], mx = a.scal[3], mn = a.scal[4];
+    const float qp_al = (float)((1 << q.nbits_alpha) - 1);
+    const float v = p.v;
+    const float t = v / scale;
+    const float rp = round_pass_value(t);
+    const float c = clamp_nan(rp, 1.f, qp_al);
+    const bool pass = (rp >= 1.f) && (rp <= qp_al);
+    const float gt = pass ? G * scale : 0.f;
+    part = make_float4(G * c, -gt * (t / scale), ((mx != mx) ? (v != v) : (v == mx)) ? 1.f : 0.f,
+                       ((mn != mn) ? (v != v) : (v == mn)) ? 1.f : 0.f);
+  }
+  return part;
+}
+
+__device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
+  const size_t nout = (size_t)g.T * g.nbw * g.nba * g.Opad;
+  if (a.wide) {
+    const size_t idx = (size_t)blk * blockDim.x + threadIdx.x;
+    const float s = (a.gaq_ready || idx >= nout) ? 0.f : sum_chunks_serial(a.ga_slab, nout, a.nchunks, idx);
+    const float4 part = idx < nout ? ga_fin(g, q, a, ga_pre(g, a, idx), idx, s) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.gapart) {
+      const float4 r = block_sum4(part, red);
+      if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = r;
+    }
+    return;
+  }
+  const size_t i0 = ((size_t)blk * a.lpr + (threadIdx.x & (a.lpr - 1))) * 4;
+  const bool mine = (int)threadIdx.x < a.lpr && i0 < nout;
+  GaPre pre[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) pre[u] = mine ? ga_pre(g, a, i0 + u) : GaPre{-1, 0.f, 0.f};
+  const float4 s = a.gaq_ready ? make_float4(0.f, 0.f, 0.f, 0.f)
+                               : reduce_chunks4(a.ga_slab, nout, a.nchunks, i0 < nout ? i0 : 0, a.lpr,
+                                                reinterpret_cast<float4*>(red));
+  if (threadIdx.x >= 64) return;
+  float4 part = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (mine) {
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 t = ga_fin(g, q, a, pre[u], i0 + u, sv[u]);
+      part.x += t.x;
+      part.y += t.y;
+      part.z += t.z;
+      part.w += t.w;
     }
   }
-  if (a.gapart && a.wide) {
-    const float4 r = block_sum4(part, red);
-    if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = r;
-  } else if (a.gapart) {
+  if (a.gapart) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       part.x += __shfl_xor(part.x, off);
@@ -386,7 +506,7 @@ __device__ inline void module_finish_block(const LsqArgs& q, const ModuleTail& a
 // The wide epilogue's last step (module_bwd_finish_wide_kernel, a.gapart set): every block sums
 // the tail blocks' first-sweep partials in the same order, then runs the second sweep of
 // alpha_cim_bwd_block over its 1024-element slice; block 0 also finishes the step sizes.
-__device__ inline void module_finish_wide_block(const LsqArgs& q, const ModuleTail& a, float* red) {
+__device__ inline void module_finish_wide_block(const LsqArgs& q, const ModuleTail& a, float* red, int blk) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int t = threadIdx.x; t < a.nga; t += blockDim.x) {
     const float4 v = reinterpret_cast<const float4*>(a.gapart)[t];
@@ -401,7 +521,7 @@ __device__ inline void module_finish_wide_block(const LsqArgs& q, const ModuleTa
   const float N = (float)((1 << q.nbits_alpha) - 2);
   const float gdiff = (r.x + r.y) / N;  // d loss / d scale, then DivBackward of (max - min) / N
   const float pmax = gdiff / r.z, pmin = -gdiff / r.w;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = blk * blockDim.x + threadIdx.x;
   if (e < q.nalpha) {
     const float v = a.alpha_cim[e];
     const float t = v / scale;
@@ -415,20 +535,7 @@ __device__ inline void module_finish_wide_block(const LsqArgs& q, const ModuleTa
     rr = rr + (ismax ? pmax : 0.f);
     a.grad_alpha_cim[e] = a.accum ? a.grad_alpha_cim[e] + rr : rr;
   }
-  if (blockIdx.x == 0) lsq_finish_block(q, a, red);
+  if (blk == 0) lsq_finish_block(q, a, red);
 }
-
-// A previous layer's finish (module_finish_block) run by block 0 of this layer's v7 grad_x
-// launch (the chained module backward, cimq_module_backward_chain): the kernel boundaries that
-// order this layer's work also order it after the previous layer's tail, so it needs no launch of
-// its own.  Works with any block size (the reductions stride by blockDim).  tail_blocks is the
-// grid of the previous layer's tail launch (host side).
-struct Carry {
-  int tail_blocks;
-  int finish;
-  Geo g;  // the previous layer's geometry
-  LsqArgs q;
-  ModuleTail a;
-};
 
 }  // namespace cimq

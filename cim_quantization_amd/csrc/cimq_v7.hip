@@ -106,19 +106,12 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
                                                             const float* __restrict__ sa_p,
                                                             const float* __restrict__ gout,
                                                             const float* __restrict__ x, float* __restrict__ gx,
-                                                            float* __restrict__ gsa_part, Carry cr) {
+                                                            float* __restrict__ gsa_part) {
   constexpr int NKS = (NBW * OBX + 1) / 2;
   constexpr int NKJ = NBW * NBA;
   constexpr bool PLS = NKJ > 10;  // plane state words (cim_fwd_v3_kernel PLF)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // the previous layer's finish (struct Carry) in block 0, dispatched first: one short block
-  // among the many of this launch (3.33 ms/step; in the last block, run while the launch drains,
-  // 3.34 ms; in grad_w's launch, which fills the chip exactly, 3.39 ms)
-  if (cr.finish && blockIdx.x == 0) {
-    module_finish_block(cr.q, cr.a, reinterpret_cast<float*>(smem));
-    return;
-  }
-  const int bid = (int)blockIdx.x - (cr.finish ? 1 : 0);
+  const int bid = (int)blockIdx.x;
   const int b = bid / v.nbands, band = bid - b * v.nbands;
   const int r0 = band * v.RB, r1 = min(g.H, r0 + v.RB);
   // output rows whose windows touch input rows [r0, r1) (pad 1, 3 kernel rows, stride SS)

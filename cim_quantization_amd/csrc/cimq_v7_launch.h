@@ -11,7 +11,7 @@ namespace cimq {
 template <int NBW, int NBA, int OBX>
 int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                  const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
-                 const Carry& carry, int parts) {
+                 int parts) {
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
@@ -29,9 +29,9 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
 #undef CIMQ_GX8
     CIMQ_TRY(set_lds(kern, p.lds_gx));
     const int slot = prof_begin(KID_GX_V8, g, s);
-    hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands + (carry.finish ? 1 : 0)), dim3(256 * np), p.lds_gx, s, g, p.v, st,
+    hipLaunchKernelGGL(kern, dim3(g.B * p.v.nbands), dim3(256 * np), p.lds_gx, s, g, p.v, st,
                        reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wcy), pp, sw, sa, gout, x, gx,
-                       reinterpret_cast<float*>(ws + W.lsq_part), carry);
+                       reinterpret_cast<float*>(ws + W.lsq_part));
     prof_end(slot, s);
     CIMQ_TRY(check_hip("cim_bwd_gx_v8"));
   }
@@ -50,13 +50,13 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
 template <int NBW, int NBA>
 int launch_v7_n(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* sw, const float* sa,
                 const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq,
-                const Carry& carry, int parts) {
+                int parts) {
   if constexpr (NBW * NBA > 10) {
-    return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);  // v7_plan: OB16 == 1
+    return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);  // v7_plan: OB16 == 1
   } else {
-    if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
-    if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
-    return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, carry, parts);
+    if (g.OB16 == 1) return launch_v7_nb<NBW, NBA, 1>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
+    if (g.OB16 == 2) return launch_v7_nb<NBW, NBA, 2>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
+    return launch_v7_nb<NBW, NBA, 4>(g, p, ctx, sw, sa, gout, x, gx, ws, s, lsq, parts);
   }
 }
 

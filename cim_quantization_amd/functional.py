@@ -346,22 +346,28 @@ def cim_conv2d_lsq_shift(x, w_q, sa, sw, alpha_q, beta, binary_mask, signed_act,
 
 
 class _ChainState:
-    """The chained module backward of one device (cimq_module_backward_chain): the epilogue the
-    last call left, the tensors it reads / writes (kept alive until it has been issued), the stream
+    """The chained module backward of one device (cimq_module_backward_chain): the epilogues the
+    calls left, the tensors each reads / writes (kept alive until it has been issued), the stream
     of the chain, and whether the end-of-backward flush is queued or a chained_epilogues() scope
     owns the flush."""
 
     def __init__(self):
         self.pending = _lib.Pending()
-        self.keep = None
+        self.keep = []
         self.stream = None
         self.queued = False
         self.scopes = 0
 
+    def add(self, bufs):
+        # a call that issued the earlier epilogues itself (a full list) leaves only its own
+        if _lib.load().cimq_pending_jobs(self.pending) <= 1:
+            self.keep = []
+        self.keep.append(bufs)
+
     def flush(self):
-        if self.keep is not None:
+        if self.keep:
             _lib.check(_lib.load().cimq_pending_flush(self.pending, self.stream), "cimq_pending_flush")
-        self.keep = None
+        self.keep = []
         self.queued = False
 
 
@@ -376,9 +382,8 @@ def _chain(dev):
 @contextlib.contextmanager
 def chained_epilogues(device=None):
     """Chain the parameter-gradient epilogues of Conv2dLSQCiM backwards across separate
-    ``backward()`` calls made inside this scope (e.g. one per layer, as bench.py does): each
-    layer's epilogue runs inside the next layer's backward kernels and the last one is flushed
-    when the scope ends.  Without a scope, a single backward pass chains its layers and flushes
+    ``backward()`` calls made inside this scope (e.g. one per layer, as bench.py does): every
+    layer's epilogue is held back and all are launched together, packed, when the scope ends.  Without a scope, a single backward pass chains its layers and flushes
     at its end (a queued autograd callback).  Applies to the in-place accumulating backward
     (GradBucket-owned layers); read the gradients only after the scope."""
     ch = _chain(torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device))
@@ -574,11 +579,11 @@ class _CimModuleConv(torch.autograd.Function):
         ws = torch.empty(max(ctx.sizes.bwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
         lib = _lib.load()
         if targets is not None and side is None and CHAIN_EPILOGUES:
-            # chained: this layer's epilogue runs inside the next layer's backward kernels (or at the
-            # flush); the previous layer's runs inside ours
+            # chained: this layer's epilogue waits in the pending list; the flush launches all of
+            # them packed into a few launches
             ch = _chain(dev)
             stream = _stream()
-            if ch.keep is not None and ch.stream != stream:
+            if ch.keep and ch.stream != stream:
                 ch.flush()
             if ch.scopes == 0 and not ch.queued:
                 torch.autograd.Variable._execution_engine.queue_callback(ch.flush)
@@ -591,7 +596,7 @@ class _CimModuleConv(torch.autograd.Function):
                                                       gaa.data_ptr(), gaw.data_ptr(),
                                                       None if gac is None else gac.data_ptr(), ws.data_ptr(),
                                                       ch.pending, stream), "cimq_module_backward_chain")
-            ch.keep = (ws, cbuf, wc, ac, gw, gaa, gaw, gac, ctx.wprep_buf)
+            ch.add((ws, cbuf, wc, ac, gw, gaa, gaw, gac, ctx.wprep_buf))
             return (gx,) + (None,) * 20
         _lib.check(lib.cimq_module_backward(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
                                             aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 10
+#define CIMQ_ABI_VERSION 11
 
 /* status codes */
 #define CIMQ_OK 0
@@ -233,20 +233,22 @@ typedef struct cimq_prepare_item {
  * re-prepared in between. */
 int cimq_module_prepare(int n, const cimq_prepare_item* items, void* stream);
 
-/* Opaque, caller-owned host memory for cimq_module_backward_chain: zero-initialise it once. */
+/* Opaque, caller-owned host memory for cimq_module_backward_chain: zero-initialise it once.
+ * 16 KB since ABI 11. */
 typedef struct cimq_pending {
-  uint64_t opaque[128];
+  uint64_t opaque[2048];
 } cimq_pending;
 
 /* cimq_module_backward for a chain of layers run back to back on ONE stream (a network's
- * backward pass): the parameter-gradient epilogue of each call (module_bwd_tail / _finish) is
- * not launched but left in ``pending``; the NEXT chained call runs it inside its own grad_x /
- * grad_w kernels as extra workgroups (or on its own first, when that layer's backward is not the
- * v7 path), and leaves its own.  cimq_pending_flush runs whatever is left.  The parameter
- * gradients of a call are therefore complete only after the next chained call or the flush has
- * been issued on the stream; every buffer the call used (ctx, ws, weight, alpha_cim, the four
- * gradient buffers) must stay valid until then.  Same arguments as cimq_module_backward;
- * CIMQ_LSQ_SKIP_TAIL is refused. */
+ * backward pass): the parameter-gradient epilogue of each call (the grad_w / grad_alpha slab
+ * sums, the LSQ and alpha_cim quantiser backwards) is not launched but left in ``pending``;
+ * cimq_pending_flush launches every pending epilogue at once, packed into two launches per up to
+ * 20 layers (since ABI 11; before, each ran inside the next call's kernels).  A call also issues
+ * the pending ones first when 32 are pending or when a pending one writes one of its gradient
+ * buffers.  The parameter gradients of a call are therefore complete only after the flush (or a
+ * later call that issued them) has been issued on the stream; every buffer the call used (ctx,
+ * ws, weight, alpha_cim, the four gradient buffers) must stay valid until then.  Same arguments
+ * as cimq_module_backward; CIMQ_LSQ_SKIP_TAIL and CIMQ_LSQ_DEFER_GW are refused. */
 int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
                                const float* x, const float* weight, const float* alpha_act,
                                const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,
@@ -254,6 +256,9 @@ int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
                                float* grad_alpha_act, float* grad_alpha_weight, float* grad_alpha_cim, void* ws,
                                cimq_pending* pending, void* stream);
 int cimq_pending_flush(cimq_pending* pending, void* stream);
+/* The number of epilogues ``pending`` holds (not yet issued).  After a chained call it is 1 when
+ * every earlier one has been issued: the caller may then release their buffers.  Since ABI 11. */
+int cimq_pending_jobs(const cimq_pending* pending);
 
 /* First-step alpha_cim initialisation (lsq.py:557-563 with get_analog_partial_sums_signed,
  * lsq.py:35-87): alpha_init[1,T,nbw,nba,1,O] = 2*mean_{b,p}|ps*sw*sa| / sqrt(Qp_adc), zeros
