@@ -370,8 +370,9 @@ static TailLaunch tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc*
   // thread (16 k blocks of 64 outputs each took 67 us for 34 MB of slab)
   const long long nout_w = (long long)g.T * g.FBT * 16 * g.Opad;
   a.wide = (a.nchunks <= 16 && nout_w >= (1 << 18) && tune("WIDE_SLAB", 1)) ? 1 : 0;
-  // otherwise float4 reads, 16-lane rows when the chunks are many (reduce_chunks4)
-  a.lpr = a.nchunks > tune("TAIL_LPR_CHUNKS", 64) ? 16 : 64;
+  // otherwise float4 reads in 64-lane rows (reduce_chunks4); 16-lane rows for the many-chunk slabs
+  // (4x the blocks, one load batch each) measured slower: 85.7 -> 92.6 us for the packed tail
+  a.lpr = a.nchunks > tune("TAIL_LPR_CHUNKS", 1 << 30) ? 16 : 64;
   const int per_blk = a.wide ? 1024 : 4 * a.lpr;
   a.nwb = cdiv(nout_w, per_blk);
   a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, per_blk) : 0;
@@ -434,14 +435,20 @@ static int pending_run(Pending* pd, hipStream_t s) {
   const int n = pd->n;
   pd->magic = 0;
   pd->n = 0;
+  // the jobs with the longest blocks (most chunks per output) first, so that the grid does not
+  // end on a round of them; the jobs are independent (pending_overlaps), their order is free
+  int ord[kPendingJobs];
+  for (int i = 0; i < n; ++i) ord[i] = i;
+  if (tune("TAIL_SORT", 1))
+    std::stable_sort(ord, ord + n, [&](int x, int y) { return pd->job[x].a.nchunks > pd->job[y].a.nchunks; });
   for (int i = 0; i < n;) {
     TailPack tp;
     tp.n = 0;
     int blk = 0;
     for (; i < n && tp.n < kTailJobs; ++i, ++tp.n) {
       tp.blk0[tp.n] = blk;
-      tp.job[tp.n] = pd->job[i];
-      blk += pd->nblk[i];
+      tp.job[tp.n] = pd->job[ord[i]];
+      blk += pd->nblk[ord[i]];
     }
     tp.blk0[tp.n] = blk;
     hipLaunchKernelGGL(module_tail_many_kernel, dim3(blk), dim3(1024), 0, s, tp);

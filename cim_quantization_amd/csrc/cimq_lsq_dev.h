@@ -118,8 +118,8 @@ __device__ inline float sum_chunks_serial(const float* __restrict__ slab, size_t
 
 // The slab sum of four consecutive outputs per lane: the block's lpr-lane rows (lpr = 16 or 64)
 // each take every nsub-th chunk, then the first row sums the rows in
-// order through LDS.  Many chunks (the per-image slabs of the fused / first-conv kernels, 256-512)
-// take lpr 16: 64 chunk rows, so one batch of loads per lane instead of four.  red: blockDim float4s.
+// order through LDS.  lpr 16 (64 chunk rows: one batch of loads per lane on the 256-512-chunk
+// slabs, 4x the blocks) measured slower than 64 for the packed tail.  red: blockDim float4s.
 __device__ inline float4 reduce_chunks4(const float* __restrict__ slab, size_t chunk_stride, int nchunks, size_t idx,
                                         int lpr, float4* red) {
   const int sub = (int)threadIdx.x / lpr, nsub = (int)blockDim.x / lpr;
