@@ -212,10 +212,19 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
     const size_t i0 = ((size_t)blk * a.lpr + (threadIdx.x & (a.lpr - 1))) * 4;
     const bool mine = (int)threadIdx.x < a.lpr && i0 < nout;
     GwPre pre[4];
+#ifdef CIMQ_EXP_TAIL_NOEPI  // attribution builds only (tools/kernel_experiment.py)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pre[u] = GwPre{-1, 0.f, 0.f};
+#else
 #pragma unroll
     for (int u = 0; u < 4; ++u) pre[u] = mine ? gw_pre(g, a, i0 + u) : GwPre{-1, 0.f, 0.f};
+#endif
+#ifdef CIMQ_EXP_TAIL_NOSLAB
+    const float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#else
     const float4 v = reduce_chunks4(a.gw_slab, nout, a.nchunks, i0 < nout ? i0 : 0, a.lpr,
                                     reinterpret_cast<float4*>(red));
+#endif
     if (threadIdx.x >= 64) return;
     float p_mul = 0.f, p_div = 0.f;
     const float nbw = (float)g.nbw;

@@ -33,6 +33,10 @@ VARIANTS = {
     "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],
     "fwd_nostagex": ["CIMQ_EXP_FWD_NOSTAGEX"],
     "fwd_nostage": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX"],
+    # the module epilogue's grad_w role: without the weight quantiser's loads / stores, without the
+    # slab sums (tools/tail_sweep.sh with CIMQ_LIB_PATH=<variant lib>)
+    "tail_noepi": ["CIMQ_EXP_TAIL_NOEPI"],
+    "tail_noslab": ["CIMQ_EXP_TAIL_NOSLAB"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
