@@ -15,6 +15,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
 ABI_VERSION = 11
 
+CIMQ_EINVAL = 1  # include/cimq.h error codes
+CIMQ_EUNSUPPORTED = 2
+CIMQ_EHIP = 3
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
 CIMQ_LSQ_ACCUMULATE_GRADS = 1

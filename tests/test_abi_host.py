@@ -155,3 +155,18 @@ def test_module_shift_supported_resnet56_shapes(lib, C, O, H, s):
     assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kw8w)) == 0
     kwx = dict(kw, input_kind=L.CIMQ_INPUT_XQ)
     assert lib.cimq_module_shift_supported(_desc(adc_variant=L.CIMQ_ADC_SHIFT_ROUND, **kwx)) == 0
+
+
+def test_pending_host_logic(lib):
+    """cimq_pending (ABI 11): a zeroed one holds no epilogue and flushes to nothing (no HIP call);
+    one that was never zeroed is refused by every entry point that takes it."""
+    p = L.Pending()
+    assert ctypes.sizeof(p) == 16384
+    assert lib.cimq_pending_jobs(p) == 0
+    assert lib.cimq_pending_flush(p, None) == 0
+    assert lib.cimq_pending_jobs(p) == 0
+    p.opaque[0] = 0x1234  # not the library's magic
+    assert lib.cimq_pending_flush(p, None) == L.CIMQ_EINVAL
+    assert b"not initialised" in lib.cimq_last_error()
+    assert lib.cimq_pending_jobs(p) == 0
+    assert lib.cimq_pending_flush(None, None) == L.CIMQ_EINVAL
