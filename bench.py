@@ -97,8 +97,8 @@ class Trainer:
         self.synced_init = False
         self.flat = self.bucket.flat
         # SGD with momentum, weight decay 1e-4 except alpha_* (examples/__init__.py:184-188), on the
-        # flat parameter / gradient buffers (dist.FlatSGD: 4 launches; torch's foreach SGD took 7
-        # launches, 57 us per step, its fused SGD 77 us)
+        # flat parameter / gradient buffers (dist.FlatSGD: one cimq_flat_sgd launch that also zeroes
+        # the gradients; torch's foreach SGD took 7 launches, 57 us per step, its fused SGD 77 us)
         from cim_quantization_amd.dist import FlatSGD
         wd = [0.0 if nm.startswith("alpha") else 1e-4 for m in layers for nm, _ in m.named_parameters()]
         self.opt = FlatSGD(self.bucket, lr=0.01, momentum=0.9, weight_decay=wd)
@@ -119,8 +119,7 @@ class Trainer:
     def finish(self):
         """gradient exchange (one RCCL all-reduce of the bucket) + SGD update."""
         self.bucket.exchange()
-        self.opt.step()
-        self.flat.zero_()
+        self.opt.step(zero_grad=True)  # the update and the gradients' zeroing in one launch
 
     def step(self, xs, gs):
         self.compute(xs, gs)

@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "cimq_profile_start",
     "cimq_profile_stop",
     "cimq_profile_read",
+    "cimq_flat_sgd",
 )
 
 KERNEL_IDS = {"fwd": 1, "bwd_gx": 2, "bwd_gw": 3, "prep_act": 4, "fwd_v7": 5, "gx_v8": 6, "gw_v7": 7, "bwd_fused": 8}
@@ -205,6 +206,9 @@ def _bind(lib):
     lib.cimq_qconv_forward.argtypes = [ctypes.POINTER(QConvDesc)] + [_VP] * 9
     lib.cimq_qconv_backward_scales.restype = ctypes.c_int
     lib.cimq_qconv_backward_scales.argtypes = [ctypes.POINTER(QConvDesc)] + [_VP] * 8
+    lib.cimq_flat_sgd.restype = ctypes.c_int
+    lib.cimq_flat_sgd.argtypes = [ctypes.c_longlong, _VP, _VP, _VP, _VP, ctypes.c_float, ctypes.c_float, ctypes.c_int,
+                                  ctypes.c_int, _VP]
     lib.cimq_profile_start.restype = ctypes.c_int
     lib.cimq_profile_start.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.cimq_profile_read.restype = ctypes.c_int

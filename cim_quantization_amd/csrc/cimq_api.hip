@@ -889,6 +889,51 @@ int cimq_alpha_init(const cimq_conv_desc* d, const float* x, const float* w_q, c
   return launch_reduce_galpha(g, c, w, 0.f, 1, sw, sa, alpha_init, s);
 }
 
+// dist.FlatSGD's update: four elements per thread (the flat buffers are 256-B aligned torch
+// allocations), the last n % 4 by thread 0 of block 0
+__global__ __launch_bounds__(256) void flat_sgd_kernel(long long n, float* __restrict__ p, float* __restrict__ g,
+                                                       float* __restrict__ buf, const float* __restrict__ wd, float lr,
+                                                       float mom, int first, int zero_grad) {
+  auto upd = [&](float pv, float gv, float bv, float w, float& po, float& bo) {
+    const float d = gv + w * pv;
+    bo = first ? d : mom * bv + d;
+    po = pv - lr * bo;
+  };
+  const long long n4 = n >> 2;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += (long long)gridDim.x * blockDim.x) {
+    const float4 pv = reinterpret_cast<const float4*>(p)[t], gv = reinterpret_cast<const float4*>(g)[t];
+    const float4 wv = reinterpret_cast<const float4*>(wd)[t];
+    const float4 bv = first ? make_float4(0.f, 0.f, 0.f, 0.f) : reinterpret_cast<const float4*>(buf)[t];
+    float4 po, bo;
+    upd(pv.x, gv.x, bv.x, wv.x, po.x, bo.x);
+    upd(pv.y, gv.y, bv.y, wv.y, po.y, bo.y);
+    upd(pv.z, gv.z, bv.z, wv.z, po.z, bo.z);
+    upd(pv.w, gv.w, bv.w, wv.w, po.w, bo.w);
+    reinterpret_cast<float4*>(p)[t] = po;
+    reinterpret_cast<float4*>(buf)[t] = bo;
+    if (zero_grad) reinterpret_cast<float4*>(g)[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (long long e = n4 << 2; e < n; ++e) {
+      upd(p[e], g[e], first ? 0.f : buf[e], wd[e], p[e], buf[e]);
+      if (zero_grad) g[e] = 0.f;
+    }
+}
+
+int cimq_flat_sgd(long long n, float* param, float* grad, float* buf, const float* wd, float lr, float momentum,
+                  int first, int zero_grad, void* stream) {
+  if (n < 0) return fail(CIMQ_EINVAL, "negative element count");
+  if (n == 0) return CIMQ_OK;
+  if (!param || !grad || !buf || !wd) return fail(CIMQ_EINVAL, "null pointer argument");
+  for (const void* q : {(const void*)param, (const void*)grad, (const void*)buf, (const void*)wd})
+    if (reinterpret_cast<uintptr_t>(q) % 16 != 0) return fail(CIMQ_EINVAL, "cimq_flat_sgd: buffers must be 16-byte aligned");
+  const long long n4 = n >> 2;
+  const int grid = (int)std::max<long long>(1, std::min<long long>(cdiv(n4, 256), 2048));
+  hipLaunchKernelGGL(flat_sgd_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, param, grad,
+                     buf, wd, lr, momentum, first ? 1 : 0, zero_grad ? 1 : 0);
+  return check_hip("flat_sgd");
+}
+
 int cimq_profile_start(int kernel_id, int max_launches) {
   Profiler& p = prof();
   std::lock_guard<std::mutex> lk(p.mu);

@@ -362,6 +362,14 @@ int cimq_profile_stop(double* total_ms, int* launches, double* algo_bytes, doubl
  * in *launches the count recorded.  Lets a caller take max(t_HBM, t_MFMA) per launch. */
 int cimq_profile_read(int cap, double* ms, double* algo_bytes, double* algo_flops, double* mfma_ops, int* launches);
 
+/* One SGD step (momentum, per-element weight decay, no dampening / Nesterov: torch.optim.SGD's
+ * update, examples/__init__.py:184-188) over n flat fp32 elements in one launch:
+ *   d = grad + wd * param;  buf = first ? d : momentum * buf + d;  param -= lr * buf
+ * (each operation rounded to fp32, no fused multiply-adds), then grad = 0 when zero_grad is set.
+ * The bench's optimizer (dist.FlatSGD) on the flat parameter / gradient buffers.  Since ABI 11. */
+int cimq_flat_sgd(long long n, float* param, float* grad, float* buf, const float* wd, float lr, float momentum,
+                  int first, int zero_grad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

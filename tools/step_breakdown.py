@@ -12,7 +12,8 @@ steps = []
 for a, b in zip(marks, marks[1:]):
     wall = int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b])
-    if busy > 0.95 * wall and b - a > 60:
+    # a training step launches 58 kernels (the forward-only graph windows: 38-40)
+    if busy > 0.95 * wall and b - a > 50:
         steps.append((a, b, wall))
 d = collections.defaultdict(float)
 cnt = collections.defaultdict(int)
@@ -22,6 +23,8 @@ for a, b, _ in steps:
         d[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         cnt[n] += 1
 ns = len(steps)
+if ns == 0:
+    sys.exit("no steady step windows found")
 print(f"{ns} steady steps, wall {sum(s[2] for s in steps) / ns / 1e3:.1f} us/step")
 for n, t in sorted(d.items(), key=lambda kv: -kv[1]):
     print(f"{t / ns:8.1f} us/step  {cnt[n] / ns:5.1f}x  {n}")
