@@ -344,7 +344,7 @@ struct TailLaunch {
 
 static TailLaunch tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc* q, const uint8_t* c, uint8_t* w,
                       const float* weight, const float* alpha_cim, float* grad_weight, float* grad_alpha_act,
-                      float* grad_alpha_weight, float* grad_alpha_cim, int gaq_ready = 0) {
+                      float* grad_alpha_weight, float* grad_alpha_cim, int gaq_ready = 0, bool packed = false) {
   const bool has_alpha = la.nbits_alpha > 0;
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
@@ -370,10 +370,12 @@ static TailLaunch tail_job(const Geo& g, const LsqArgs& la, const cimq_lsq_desc*
   // thread (16 k blocks of 64 outputs each took 67 us for 34 MB of slab)
   const long long nout_w = (long long)g.T * g.FBT * 16 * g.Opad;
   a.wide = (a.nchunks <= 16 && nout_w >= (1 << 18) && tune("WIDE_SLAB", 1)) ? 1 : 0;
-  // otherwise float4 reads in 64-lane rows (reduce_chunks4); 16-lane rows for the many-chunk slabs
-  // (4x the blocks, one load batch each) measured slower: 85.7 -> 92.6 us for the packed tail
-  a.lpr = a.nchunks > tune("TAIL_LPR_CHUNKS", 1 << 30) ? 16 : 64;
-  const int per_blk = a.wide ? 1024 : 4 * a.lpr;
+  // otherwise, in a launch packed with the other layers' epilogues (cimq_pending_flush), float4
+  // reads in 64-lane rows, 256 outputs per block (reduce_chunks4; 16-lane rows there: 85.7 -> 92.6
+  // us); alone, one output per lane, 64 per block, so that a small layer still spreads over the chip
+  // (a layer's tail 6.8 us against 9.1 with the float4 rows, cfg4)
+  a.lpr = packed ? tune("TAIL_LPR_PACKED", 64) : tune("TAIL_LPR_SINGLE", 0);
+  const int per_blk = a.wide ? 1024 : a.lpr == 0 ? 64 : 4 * a.lpr;
   a.nwb = cdiv(nout_w, per_blk);
   a.nga = has_alpha ? cdiv((long long)g.T * g.nbw * g.nba * g.Opad, per_blk) : 0;
   a.napart = act_parts(g);
@@ -691,7 +693,7 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
     // the epilogue joins the pending ones: cimq_pending_flush (or a full list, or a layer whose
     // gradient buffers a pending one writes) launches them all, packed
     const TailLaunch j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
-                             grad_alpha_cim);
+                                  grad_alpha_cim, 0, true);
     if (pend->magic == kPendingMagic && (pend->n == kPendingJobs || pending_overlaps(pend, j.a)))
       CIMQ_TRY(pending_run(pend, s));
     if (pend->magic != kPendingMagic) pend->n = 0;

@@ -91,7 +91,8 @@ struct ModuleTail {
   uint8_t wide;       // few chunks, many outputs (the dense path): one output per thread of a 1024-thread
                       // block (nwb / nga count such blocks), the chunks summed in order by that thread
   uint8_t lpr;        // not wide: float4 slab reads, lpr lanes (16 or 64) x 4 outputs per block and
-                      // 1024 / lpr chunk groups (reduce_chunks4); nwb / nga count such blocks
+                      // 1024 / lpr chunk groups (reduce_chunks4); 0: one output per lane, 64 per
+                      // block, 16 chunk groups (reduce_chunks); nwb / nga count such blocks
 };
 // alpha_cim sizes the one-block epilogue keeps in registers (module_finish_block); larger ones
 // (the QuantLinear layers: T * nbw * nba * O = 131072 at 1024 -> 1024 w4a4) take the wide path:
@@ -208,6 +209,24 @@ __device__ inline void gw_fin(const LsqArgs& q, const ModuleTail& a, const GwPre
 __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleTail& a, int blk, float* red) {
   const size_t rows = (size_t)g.T * g.FBT * 16;
   const size_t nout = rows * g.Opad;
+  if (!a.wide && a.lpr == 0) {  // scalar: one output per lane of the first wave, 64 per block (reduce_chunks)
+    const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
+    const GwPre pre = (threadIdx.x < 64 && idx < nout) ? gw_pre(g, a, idx) : GwPre{-1, 0.f, 0.f};
+    const float vsum = reduce_chunks(a.gw_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+    if (threadIdx.x >= 64) return;
+    float p_mul = 0.f, p_div = 0.f;
+    gw_fin(q, a, pre, vsum, (float)g.nbw, p_mul, p_div);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      p_mul += __shfl_xor(p_mul, o);
+      p_div += __shfl_xor(p_div, o);
+    }
+    if (threadIdx.x == 0) {
+      a.wpart[2 * blk] = p_mul;
+      a.wpart[2 * blk + 1] = p_div;
+    }
+    return;
+  }
   if (!a.wide) {  // nout % 16 == 0 (Opad)
     const size_t i0 = ((size_t)blk * a.lpr + (threadIdx.x & (a.lpr - 1))) * 4;
     const bool mine = (int)threadIdx.x < a.lpr && i0 < nout;
@@ -311,6 +330,24 @@ __device__ inline void galpha_role(const Geo& g, const LsqArgs& q, const ModuleT
     if (a.gapart) {
       const float4 r = block_sum4(part, red);
       if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = r;
+    }
+    return;
+  }
+  if (a.lpr == 0) {  // scalar, as gw_lsq_role
+    const size_t idx = (size_t)blk * 64 + (threadIdx.x & 63);
+    const GaPre pre = (threadIdx.x < 64 && idx < nout) ? ga_pre(g, a, idx) : GaPre{-1, 0.f, 0.f};
+    const float sv = a.gaq_ready ? 0.f : reduce_chunks(a.ga_slab, nout, a.nchunks, idx < nout ? idx : 0, red);
+    if (threadIdx.x >= 64) return;
+    float4 part = ga_fin(g, q, a, pre, idx, sv);
+    if (a.gapart) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        part.x += __shfl_xor(part.x, off);
+        part.y += __shfl_xor(part.y, off);
+        part.z += __shfl_xor(part.z, off);
+        part.w += __shfl_xor(part.w, off);
+      }
+      if (threadIdx.x == 0) reinterpret_cast<float4*>(a.gapart)[blk] = part;
     }
     return;
   }

@@ -74,6 +74,8 @@ def test_bench_graph_composition_vs_oracle(cuda_device, monkeypatch):
                                   1.0 / math.sqrt(x.numel() * qp_a))
         t_w = _lsq_scalar_terms(m.weight.detach().cpu().numpy(), d["w_q"].grad.numpy(), d["sw"].item(), qn_w, qp_w,
                                 1.0 / math.sqrt(m.weight.numel() * qp_w))
-        assert abs(float(mine["alpha_act"]) - om.alpha_act.grad.item()) <= 1e-5 * t_act, (name, "alpha_act")
-        assert abs(float(mine["alpha_weight"]) - om.alpha_weight.grad.item()) <= 1e-5 * t_w, (name, "alpha_weight")
+        assert abs(float(np.asarray(mine["alpha_act"]).reshape(-1)[0]) - om.alpha_act.grad.item()) <= 1e-5 * t_act, \
+            (name, "alpha_act")
+        assert abs(float(np.asarray(mine["alpha_weight"]).reshape(-1)[0]) - om.alpha_weight.grad.item()) <= 1e-5 * t_w, \
+            (name, "alpha_weight")
         assert (c.adc != 0).mean() > 0.05, (name, "codes must vary for the check to bite")

@@ -1,7 +1,8 @@
 """GPU: the chained module backward (cimq_module_backward_chain): each layer's parameter-gradient
 epilogue is held in the pending list and the flush launches them all, packed two launches per up
 to 20 layers.  The gradients must match the unchained backward: grad_x bit for bit (same
-kernels), the parameter gradients too (the packed kernels run the same per-block reductions)."""
+kernels), the parameter gradients to fp32 summation order (the packed launch sums each slab in
+float4 rows of 256 outputs per block, a layer's own launch one output per lane, 64 per block)."""
 import pytest
 import torch
 
@@ -9,6 +10,12 @@ pytestmark = pytest.mark.gpu
 
 # (C, O, H, stride, bits): w8a8 first conv, w3a3 stride 1 / 2, a 16x16 layer, and a 12x12 one
 # (non-power-of-two width: the general backward, so the chain flushes before it)
+def _close(a, b):
+    """elementwise within the reordering of fp32 sums: 1e-5 relative, plus 1e-6 of the largest"""
+    tol = 1e-5 * b.abs() + 1e-6 * b.abs().max()
+    assert ((a - b).abs() <= tol).all(), ((a - b).abs() - tol).max().item()
+
+
 SPECS = [(3, 16, 32, 1, 8), (16, 16, 32, 1, 3), (16, 32, 32, 2, 3), (32, 32, 16, 1, 3), (32, 32, 12, 1, 3),
          (32, 64, 16, 2, 3), (64, 64, 8, 1, 3)]
 
@@ -70,7 +77,7 @@ def test_chained_equals_unchained_per_layer_backwards(cuda_device):
     gx_ch, flat_ch = _step(la, ba, xs2, gs2, True)
     for i, (a, b) in enumerate(zip(gx_ch, gx_ref)):
         assert torch.equal(a, b), i  # same kernels, fixed-order sums
-    assert torch.equal(flat_ch, flat_ref)  # the packed epilogue runs the same per-block sums
+    _close(flat_ch, flat_ref)
     assert torch.isfinite(flat_ch).all()
 
 
@@ -94,7 +101,7 @@ def _deep(dev, n, shared):
 def test_chain_packs_and_capacity(cuda_device, n, shared):
     """35 layers: a list full at 32 issued by the 33rd call (tail packs of 20 and 12), then 3 at the flush;
     one layer run 4 times: each call issues the pending epilogue that writes the same gradients.
-    Every gradient bit for bit against the unchained backward."""
+    grad_x bit for bit against the unchained backward, the parameter gradients to summation order."""
     import cim_quantization_amd.functional as F
     g = torch.Generator().manual_seed(4)
     xs = [torch.randn(2, 16, 8, 8, generator=g).relu().to(cuda_device) for _ in range(n)]
@@ -111,7 +118,7 @@ def test_chain_packs_and_capacity(cuda_device, n, shared):
         runs.append((gx, flat))
     for a, b in zip(runs[0][0], runs[1][0]):
         assert torch.equal(a, b)
-    assert torch.equal(runs[0][1], runs[1][1])
+    _close(runs[1][1], runs[0][1])
     assert F._chain(torch.device(cuda_device)).keep == []
 
 
@@ -145,7 +152,7 @@ def test_chain_inside_one_backward_pass(cuda_device):
             F.CHAIN_EPILOGUES = True
         torch.cuda.synchronize()
         outs.append(bk.flat.detach().clone())
-    assert torch.equal(outs[0], outs[1])
+    _close(outs[0], outs[1])
 
 
 def test_overlapped_param_half_equals_single_stream(cuda_device):
