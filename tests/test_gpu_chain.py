@@ -176,3 +176,38 @@ def test_overlapped_param_half_equals_single_stream(cuda_device):
         assert torch.equal(a, b), i
     assert torch.equal(flat_ov, flat_ref)
     assert torch.isfinite(flat_ov).all()
+
+
+def test_chain_with_wide_alpha_dense_layers(cuda_device):
+    """Two QuantLinear-shaped layers (BASELINE cfg5's 1024 -> 1024 w4a4, xbar 128, the dense path) in
+    one chain: alpha_cim has T * nbw * nba * O = 131072 elements, so their packed epilogues take the
+    wide tail (one output per thread) and the multi-block finish (module_finish_wide_block per job)."""
+    import cim_quantization_amd._modules as my_nn
+    import cim_quantization_amd.functional as F
+    from cim_quantization_amd.dist import GradBucket
+    g = torch.Generator().manual_seed(8)
+    xs = [torch.randn(256, 1024, 1, 1, generator=g).relu().to(cuda_device) for _ in range(2)]
+    gs = [(torch.randn(256, 1024, 1, 1, generator=g) / 512.0).to(cuda_device) for _ in range(2)]
+    runs = []
+    for chained in (False, True):
+        torch.manual_seed(4)
+        ms = []
+        for _ in range(2):
+            m = my_nn.Conv2dLSQCiM(1024, 1024, 1, 1, 0, bias=False, nbits_w=4, nbits_a=4, nbits_alpha=8, xbar=128,
+                                   adcbits=1.5)
+            torch.nn.init.kaiming_normal_(m.weight)
+            ms.append(m.to(cuda_device).train())
+        bucket = GradBucket([p for m in ms for p in m.parameters()])
+        bucket.own(ms)
+        _step(ms, bucket, xs, gs, False)  # initialising step
+        F.CHAIN_EPILOGUES = chained
+        try:
+            gx, flat = _step(ms, bucket, xs, gs, chained)
+        finally:
+            F.CHAIN_EPILOGUES = True
+        assert ms[0].alpha_cim.numel() == 8 * 4 * 4 * 1024
+        runs.append((gx, flat))
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert torch.equal(a, b)
+    _close(runs[1][1], runs[0][1])
+    assert torch.isfinite(runs[1][1]).all()
