@@ -84,9 +84,20 @@ class Trainer:
     """fwd+bwd over the CiM layers, flat-bucket gradient all-reduce, SGD (examples/__init__.py:184-188:
     alpha_* excluded from weight decay)."""
 
-    def __init__(self, layers, world):
+    def __init__(self, layers, world, segments=None):
         from cim_quantization_amd.dist import GradBucket
         self.layers, self.world = layers, world
+        # the step in segments of consecutive layers (world > 1: three): at the end of a segment its
+        # layers' parameter-gradient epilogues are flushed and their slice of the bucket goes out
+        # (GradBucket.exchange_segment) while the next segment computes; one segment at world 1
+        nseg = (3 if world > 1 else 1) if segments is None else segments
+        nseg = max(1, min(nseg, len(layers)))
+        cut = [round(i * len(layers) / nseg) for i in range(nseg + 1)]
+        self.segments = [(cut[i], cut[i + 1]) for i in range(nseg)]
+        offs = [0]
+        for m in layers:
+            offs.append(offs[-1] + sum(p.numel() for p in m.parameters()))
+        self.seg_hi = [offs[b] for _, b in self.segments]  # bucket end of each segment's gradients
         self.bucket = GradBucket([p for m in layers for p in m.parameters()])  # one all-reduce per step
         # the layers add their grads straight into the bucket; with OVERLAP their parameter-gradient
         # half (grad_w + epilogue) runs on the bucket's second stream (GradBucket.own(overlap=True))
@@ -104,17 +115,26 @@ class Trainer:
         self.opt = FlatSGD(self.bucket, lr=0.01, momentum=0.9, weight_decay=wd)
         self.bucket_mb = self.bucket.nbytes / 1e6
 
-    def compute(self, xs, gs):
-        """fwd + bwd of every layer; gradients accumulate into the flat bucket.  Each layer's
-        parameter-gradient epilogue is held back (the chained module backward,
-        functional.chained_epilogues) and all 19 run packed at the scope's end."""
+    def compute_segment(self, k, xs, gs):
+        """fwd + bwd of segment ``k``'s layers; gradients accumulate into the flat bucket.  Each
+        layer's parameter-gradient epilogue is held back (the chained module backward,
+        functional.chained_epilogues) and the segment's run packed at the scope's end."""
         from cim_quantization_amd.functional import chained_epilogues, prepare_weights
-        # the weight side of all 19 prologues in one launch, ahead of the forwards
-        prepare_weights(self.layers)
+        if k == 0:
+            # the weight side of all 19 prologues in one launch, ahead of the forwards
+            prepare_weights(self.layers)
+        a, b = self.segments[k]
         with chained_epilogues():
-            for m, x, gy in zip(self.layers, xs, gs):
+            for m, x, gy in zip(self.layers[a:b], xs[a:b], gs[a:b]):
                 m(x).backward(gy)
         self.bucket.join()  # the parameter-gradient epilogues are part of the step
+
+    def compute(self, xs, gs, exchange=False):
+        """Every segment; ``exchange``: send each finished segment's gradients on (world > 1)."""
+        for k in range(len(self.segments)):
+            self.compute_segment(k, xs, gs)
+            if exchange:
+                self.bucket.exchange_segment(self.seg_hi[k])
 
     def finish(self):
         """gradient exchange (one RCCL all-reduce of the bucket) + SGD update."""
@@ -122,7 +142,7 @@ class Trainer:
         self.opt.step(zero_grad=True)  # the update and the gradients' zeroing in one launch
 
     def step(self, xs, gs):
-        self.compute(xs, gs)
+        self.compute(xs, gs, exchange=self.synced_init)
         if not self.synced_init:
             self.bucket.broadcast_from(0, self.layers)  # rank 0's initialised alpha_* / signed_act
             self.synced_init = True
@@ -134,20 +154,26 @@ class Trainer:
                 m(x)
 
     def capture(self, xs, gs):
-        """Record fwd+bwd of all layers as one HIP graph: a step is then one graph launch plus the
-        exchange and the update, instead of ~50 host-side kernel launches per layer."""
+        """Record fwd+bwd of all layers as HIP graphs, one per segment: a step is then one graph
+        launch per segment (each followed by its gradients' exchange at world > 1) plus the
+        update, instead of ~50 host-side kernel launches per layer."""
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             self.compute(xs, gs)  # allocator / autograd warm-up on the capture stream
             self.flat.zero_()
         torch.cuda.current_stream().wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.compute(xs, gs)
+        self.graphs = []
+        for k in range(len(self.segments)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.compute_segment(k, xs, gs)
+            self.graphs.append(g)
 
     def step_graph(self, xs, gs):
-        self.graph.replay()
+        for k, g in enumerate(self.graphs):
+            g.replay()
+            self.bucket.exchange_segment(self.seg_hi[k])
         self.finish()
 
     def capture_forward(self, xs):
@@ -618,7 +644,7 @@ def main():
         "data": "synthetic (random-init weights, randn / relu(randn) activations of the layer shapes)",
         "config": {"workload": "resnet20_w3a3_all_19_cim_convs_fwd_bwd_sgd", "global_batch": args.batch * world,
                    "per_gpu_batch": args.batch, "xbar": XBAR, "adc_bits": ADC, "first_layer": "w8a8",
-                   "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3),
+                   "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3), "exchange_segments": len(tr.segments),
                    "launch": "hip_graph" if graph else "eager"},
         "roofline": dict(roof, kernel=_lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]] + " (every instantiation the "
                          "19 layers launch)", avg_launch_us=kt.total_ms / nl * 1e3, pmc_source=pmc_source),

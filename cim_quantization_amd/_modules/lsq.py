@@ -181,7 +181,13 @@ class _HostFlags:
     in-place write to them -- load_state_dict, dist.GradBucket.broadcast_from, torch DDP's buffer
     broadcast from rank 0 before every forward (train.py:232 wraps the model in DDP) -- bumps the counter
     and the next forward re-reads them, so a rank follows rank 0's buffers as the reference does.  Writes
-    through ``.data`` (which bypass the counter) update the cache alongside."""
+    through ``.data`` (which bypass the counter) update the cache alongside.
+
+    Cost under torch DDP with ``broadcast_buffers=True`` (its default): the per-forward buffer broadcast
+    bumps the counters on every step, so every module re-reads its flags with a blocking ``.item()`` per
+    forward -- the device sync this cache exists to avoid.  The buffers only change in the first
+    (initialising) step, so prefer ``dist.GradBucket`` (one exchange per step, broadcast_from(0) after the
+    first step) or DDP with ``broadcast_buffers=False`` after that step."""
 
     _state_cache = None
     _state_key = None

@@ -691,7 +691,10 @@ static int module_backward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   if (nparts != act_parts(g)) return fail(CIMQ_EINVAL, "internal: act-LSQ partial count mismatch");
   if (pend) {
     // the epilogue joins the pending ones: cimq_pending_flush (or a full list, or a layer whose
-    // gradient buffers a pending one writes) launches them all, packed
+    // gradient buffers a pending one writes) launches them all, packed.  Until then this layer's
+    // ws (its grad_w slabs: B per-image slabs on the fused / first-conv paths, ~37.7 MB for a
+    // 64-channel ResNet-20 layer at B = 256) stays in use: the chain's peak memory is up to
+    // kPendingJobs workspaces (cimq.h states it; bench.Trainer flushes per segment at world > 1)
     const TailLaunch j = tail_job(g, la, q, c, w, weight, alpha_cim, grad_weight, grad_alpha_act, grad_alpha_weight,
                                   grad_alpha_cim, 0, true);
     if (pend->magic == kPendingMagic && (pend->n == kPendingJobs || pending_overlaps(pend, j.a)))

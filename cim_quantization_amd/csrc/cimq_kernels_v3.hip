@@ -540,7 +540,14 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
       const int ksn = (min(g.xbar, g.K - i * g.xbar) + 63) >> 6;  // K-steps holding data in tile i
       v4i xs[NBP][KS];
       // (the fast path runs every K-step: ptab and the weight operand are zero past the tile)
+#ifdef CIMQ_EXP_FWD_NOGATHER  // attribution builds only: operands without the LDS gather
+#pragma unroll
+      for (int j = 0; j < NBP; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) xs[j][ks] = v4i{lane + mt, j + i, ks, rb};
+#else
       gather_xs<NBP, KS>(patch, rb, ptab + i * KS * 64, g4, xs, (CST > 0 && !literal && std8) ? KS : ksn);
+#endif
       const v4i* wt = wfl + (size_t)tt * g.nbw * NOB * KS * 64;
       const int4* pt = prm + (size_t)tt * nkj * NOB * 16;
       const float* ct = cfl + (size_t)tt * nkj * NOB * 16;
@@ -613,6 +620,18 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                 const float cf = ct[pcol];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
+#ifdef CIMQ_EXP_FWD_NOADC  // attribution builds only: no ADC, no state bits
+                  acc[ob][r] += (float)(ps[j][r] + pv.x) * cf;
+                  continue;
+#endif
+#ifdef CIMQ_EXP_FWD_NOSTATE  // attribution builds only: the ADC without the state bits
+                  {
+                    const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
+                    const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
+                    acc[ob][r] += adc3(cf, mhi, mlo);
+                    continue;
+                  }
+#endif
                   const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
                   const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
                   const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(ps[j][r] - pv.z) <= (unsigned)pv.w);
@@ -729,7 +748,11 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
           }
         }
       }
+#if defined(CIMQ_EXP_FWD_NOSTATE) || defined(CIMQ_EXP_FWD_NOADC)
+      if (false) {
+#else
       if (CST && WST) {
+#endif
 #pragma unroll
         for (int ob = 0; ob < OBM; ++ob) {
           const int o = (og * OBM + ob) * 16 + r16;

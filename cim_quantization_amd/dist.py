@@ -56,6 +56,7 @@ class GradBucket:
         self.nbytes = n * 4
         self.reattached = 0  # gradients found detached from the bucket (diagnostic)
         self.side = None  # stream of the overlapped parameter-gradient epilogues (own(overlap=True))
+        self._works, self._sent = [], 0  # segments already in flight (exchange_segment)
         self._attach()
 
     def _attach(self):
@@ -102,13 +103,35 @@ class GradBucket:
                 v.copy_(g.detach().reshape(v.shape))
             p.grad = v
 
+    def exchange_segment(self, hi, group=None):
+        """Start summing ``flat[sent:hi]`` over the ranks of ``group`` without waiting for it: the
+        gradients of the layers whose backward (and epilogue) has finished, while the backward of
+        the next layers runs.  Segments go out in bucket order, each from where the last one ended;
+        ``exchange()`` sends the rest, waits for all of them and averages.  On RCCL the collective
+        runs on the process group's stream, ordered after the work already on the current stream,
+        so the next segment's kernels overlap it.  Each element is reduced by one collective whatever
+        the segmentation: with two ranks the sum is bit-identical to the single-bucket exchange
+        (fp32 addition commutes); with more, the ring's order of additions can differ in the last
+        bit.  No-op for a single process."""
+        if _world(group) <= 1 or hi <= self._sent:
+            return
+        self.join()
+        self.sync_views()
+        self._works.append(dist.all_reduce(self.flat[self._sent:hi], group=group, async_op=True))
+        self._sent = hi
+
     def exchange(self, group=None):
-        """Average the bucket over the ranks of ``group`` (no-op for a single process)."""
+        """Average the bucket over the ranks of ``group`` (no-op for a single process): the part no
+        ``exchange_segment`` sent, then the wait for every segment, then one scale."""
         self.join()
         self.sync_views()
         world = _world(group)
         if world > 1:
-            dist.all_reduce(self.flat, group=group)
+            if self._sent < self.flat.numel():
+                dist.all_reduce(self.flat[self._sent:], group=group)
+            for w in self._works:
+                w.wait()
+            self._works, self._sent = [], 0
             self.flat.mul_(1.0 / world)
 
     def zero(self):

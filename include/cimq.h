@@ -242,13 +242,18 @@ typedef struct cimq_pending {
 /* cimq_module_backward for a chain of layers run back to back on ONE stream (a network's
  * backward pass): the parameter-gradient epilogue of each call (the grad_w / grad_alpha slab
  * sums, the LSQ and alpha_cim quantiser backwards) is not launched but left in ``pending``;
- * cimq_pending_flush launches every pending epilogue at once, packed into two launches per up to
- * 20 layers (since ABI 11; before, each ran inside the next call's kernels).  A call also issues
- * the pending ones first when 32 are pending or when a pending one writes one of its gradient
- * buffers.  The parameter gradients of a call are therefore complete only after the flush (or a
- * later call that issued them) has been issued on the stream; every buffer the call used (ctx,
- * ws, weight, alpha_cim, the four gradient buffers) must stay valid until then.  Same arguments
- * as cimq_module_backward; CIMQ_LSQ_SKIP_TAIL and CIMQ_LSQ_DEFER_GW are refused. */
+ * cimq_pending_flush launches every pending epilogue at once, packed: ceil(n/20) slab-sum (tail)
+ * launches, the jobs sorted by slab count, then ceil(n/24) finish launches (since ABI 11; before,
+ * each ran inside the next call's kernels).  A call also issues the pending ones first when 32 are
+ * pending or when a pending one writes one of its gradient buffers.  The parameter gradients of a
+ * call are therefore complete only after the flush (or a later call that issued them) has been
+ * issued on the stream; every buffer the call used (ctx, ws, weight, alpha_cim, the four gradient
+ * buffers) must stay valid and unreused until then -- in particular ``ws`` must not be handed to
+ * another chained call before that.  Memory: each pending layer keeps its workspace alive, and a
+ * workspace holds the layer's grad_w slabs (one per image on the fused / first-conv paths: about
+ * 37.7 MB for a 64-channel ResNet-20 layer at B = 256), so the chain's peak is up to 32 workspaces;
+ * flush more often (e.g. per segment of layers, as bench.Trainer does at world > 1) to bound it.
+ * Same arguments as cimq_module_backward; CIMQ_LSQ_SKIP_TAIL and CIMQ_LSQ_DEFER_GW are refused. */
 int cimq_module_backward_chain(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* grad_out,
                                const float* x, const float* weight, const float* alpha_act,
                                const float* alpha_weight, const float* alpha_cim, const int8_t* binary_mask,

@@ -77,6 +77,41 @@ def test_bucket_exchange_world2_gloo():
     assert out[0] == (0.0, 2) and out[1] == (0.0, 2)
 
 
+def _segment_worker(rank, world, port, out):
+    _init(rank, world, port)
+    try:
+        from cim_quantization_amd.dist import GradBucket
+        torch.manual_seed(7)
+        params = [torch.nn.Parameter(torch.zeros(n)) for n in (1000, 1, 333, 4096, 17, 1)]
+        seg, one = GradBucket(params), GradBucket(params)
+        g = torch.Generator().manual_seed(31 + rank)
+        vals = torch.randn(seg.flat.numel(), generator=g) * torch.logspace(-6, 3, seg.flat.numel()).flip(0)
+        seg.flat.copy_(vals)
+        one.flat.copy_(vals)
+        # three segments in bucket order (bench.Trainer's layer-segment cut), the rest by exchange()
+        for hi in (1001, 1334, 5430):
+            seg.exchange_segment(hi)
+        seg.exchange_segment(1001)  # a segment already sent is a no-op
+        seg.exchange()
+        one.exchange()
+        gathered = [torch.zeros_like(vals) for _ in range(world)]
+        dist.all_gather(gathered, vals)
+        out[rank] = (torch.equal(seg.flat, one.flat), float((one.flat - sum(gathered) / world).abs().max()),
+                     len(seg._works), seg._sent)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_segmented_exchange_bit_identical_world2_gloo():
+    """GradBucket.exchange_segment (bench.Trainer at world > 1: each finished segment's gradients go
+    out while the next segment computes) gives the single-bucket exchange bit for bit at two ranks."""
+    out = _run(_segment_worker)
+    for rank in (0, 1):
+        same, err, works, sent = out[rank]
+        assert same and err == 0.0 and works == 0 and sent == 0, out[rank]
+
+
 def _broadcast_worker(rank, world, port, out):
     _init(rank, world, port)
     try:

@@ -4,9 +4,11 @@ two processes share the one GPU, torch.distributed on gloo over device tensors.
 * bench.Trainer's real step -- prepare_weights, the chained module epilogues, GradBucket.own,
   broadcast_from and FlatSGD -- on three ResNet-20 layer shapes (the w8a8 first conv, a 16-channel
   32x32 and a 64-channel 8x8 layer) at batch 64 per rank: each rank's local bucket matches the CPU
-  module oracle run on the same state and data (normwise 1e-5 per tensor parameter; the two scalar
-  step sizes within 1e-5 of their sum of |terms|), the exchanged bucket is the mean of the two
-  ranks' buckets and of the two ranks' oracle gradients (1e-5 of the mean of |terms|), and after
+  module oracle run on the same state and data (every element within 1e-5 of max(|ref|, its sum of
+  |terms|): grad_w from the oracle's absolute re-run, grad_alpha_cim through conftest.alpha_cim_terms;
+  the two scalar step sizes within 1e-5 of their sum of |terms|), the exchanged bucket is the mean of
+  the two ranks' buckets and of the two ranks' oracle gradients (elementwise, 1e-5 of the mean of the
+  ranks' |terms|), and after
   three steps every parameter is bit-identical across the ranks;
 * bench.py's own world > 1 branch, launched by torch.distributed.run with the gloo backend.
 
@@ -62,7 +64,11 @@ def _oracle_grads(layers, xs, gs):
     the sums of |terms| of the two step-size gradients."""
     import math
 
+    import numpy as np
+
+    from conftest import alpha_cim_terms
     from oracle import cim_module_oracle as cmo
+    from oracle import cim_oracle as co
     res = []
     for (name, c, o, h, s, nb), m, x, g in zip(LAYERS, layers, xs, gs):
         om = cmo.OracleConv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
@@ -71,7 +77,22 @@ def _oracle_grads(layers, xs, gs):
         om.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()}, strict=False)
         om.train()
         xc = x.detach().cpu()
-        om(xc).backward(g.detach().cpu())
+        box = {}
+        real = co.cim_forward
+
+        def rec(*a, **k):
+            k["return_debug"] = True
+            out, c = real(*a, **k)
+            box["c"] = c
+            return out, c
+        cmo.co.cim_forward = rec
+        try:
+            om(xc).backward(g.detach().cpu())
+        finally:
+            cmo.co.cim_forward = real
+        gb = g.detach().cpu().numpy()
+        g_bpo = np.ascontiguousarray(gb.reshape(gb.shape[0], o, -1).transpose(0, 2, 1))
+        _, aw, aa = co.cim_backward(box["c"], g_bpo, absolute=True)
         d = om.dbg
         (qn_a, qp_a), (qn_w, qp_w) = d["qa"], d["qw"]
         w = om.weight.detach().numpy()
@@ -79,6 +100,10 @@ def _oracle_grads(layers, xs, gs):
                                          1.0 / math.sqrt(xc.numel() * qp_a)),
                  "alpha_weight": _lsq_terms(w, d["w_q"].grad.numpy(), d["sw"].item(), qn_w, qp_w,
                                             1.0 / math.sqrt(w.size * qp_w))}
+        # elementwise sums of |terms| of the tensor gradients: grad_w (the STE passes d loss / d w_q), and
+        # grad_alpha_cim through the alpha quantiser (conftest.alpha_cim_terms)
+        terms["weight"] = torch.from_numpy(aw.reshape(w.shape))
+        terms["alpha_cim"] = torch.from_numpy(alpha_cim_terms(om.alpha_cim.detach().numpy(), aa))
         res.append(({n: p.grad.detach().clone() for n, p in om.named_parameters()}, terms))
     return res
 
@@ -104,13 +129,19 @@ def _trainer_worker(rank, world, port, out):
         errs = []
         for m, (r, tt) in zip(layers, ref):
             for n, p in m.named_parameters():
-                d = (p.grad.detach().cpu() - r[n]).abs().max().item()
-                # normwise 1e-5; the two scalar step sizes (sums over the whole batch): 1e-5 of their terms
-                errs.append((n, d / (tt[n] if p.numel() == 1 else r[n].abs().max().item() + 1e-30)))
+                d = (p.grad.detach().cpu().double() - r[n].double()).abs()
+                # elementwise 1e-5 of max(|ref|, sum of |terms|); the two scalar step sizes (sums over the
+                # whole batch): 1e-5 of their terms
+                if p.numel() == 1:
+                    errs.append((n, d.max().item() / tt[n]))
+                else:
+                    scale = torch.maximum(r[n].double().abs(), tt[n].double().reshape(r[n].shape))
+                    errs.append((n, (d / (scale + 1e-30)).max().item()))
         ref_flat = torch.cat([r[n].reshape(-1) for m, (r, _) in zip(layers, ref) for n, _ in m.named_parameters()])
         # per parameter of the flat bucket: the scalar's sum of |terms| (else 0), for the exchanged check
-        t_flat = torch.cat([torch.full((p.numel(),), float(tt[n]) if p.numel() == 1 else 0.0, dtype=torch.float64)
-                            for m, (_, tt) in zip(layers, ref) for n, p in m.named_parameters()])
+        t_flat = torch.cat([torch.full((p.numel(),), float(tt[n]), dtype=torch.float64) if p.numel() == 1
+                            else tt[n].reshape(-1).double() for m, (_, tt) in zip(layers, ref)
+                            for n, p in m.named_parameters()])
         t_all = [torch.zeros_like(t_flat) for _ in range(world)]
         dist.all_gather(t_all, t_flat)
         t_mean = sum(t_all) / world
@@ -130,9 +161,10 @@ def _trainer_worker(rank, world, port, out):
         for m in layers:
             for _, p in m.named_parameters():
                 k = p.numel()
-                seg, rs, ra = exch[off:off + k], mean_ref[off:off + k], abs_ref[off:off + k]
-                scale = float(t_mean[off]) if k == 1 else ra.max().item() + 1e-30
-                exch_err = max(exch_err, (seg - rs).abs().max().item() / scale)
+                seg, rs, ra = exch[off:off + k].double(), mean_ref[off:off + k].double(), abs_ref[off:off + k]
+                # elementwise: the mean of the ranks' |terms| (and of their |ref|)
+                scale = torch.maximum(ra.double(), t_mean[off:off + k]) + 1e-30
+                exch_err = max(exch_err, ((seg - rs).abs() / scale).max().item())
                 off += k
         tr.opt.step()
         tr.flat.zero_()

@@ -1,7 +1,7 @@
 """GPU parity of the exact composition bench.py times: the 19 ResNet-20 CiM
 layers at batch 256 in ``bench.Trainer`` -- the weight side of all layers prepared in one launch
 (``prepare_weights``), the chained parameter-gradient epilogues, gradients accumulated in place into
-the flat ``GradBucket`` -- captured as one HIP graph and replayed.  The bucket's gradients of the w8a8
+the flat ``GradBucket`` -- captured in three segment graphs (as at world > 1) and replayed.  The bucket's gradients of the w8a8
 first conv, a 16-channel layer, the first stride-2 transition and a 64-channel layer are compared with
 the module oracle (oracle/cim_module_oracle.py, lsq.py:511-588) run on the same inputs and parameters,
 elementwise against the sum of |terms| like tests/test_gpu_fullsize.py.
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import rel_err
+from conftest import alpha_cim_terms, rel_err
 from oracle import cim_module_oracle as cmo
 from oracle import cim_oracle as co
 from test_gpu_fullsize import _capture_oracle_ctx, _lsq_scalar_terms
@@ -26,12 +26,15 @@ def test_bench_graph_composition_vs_oracle(cuda_device, monkeypatch):
     import bench
     names = [r[0] for r in bench.RESNET20]
     layers, xs, gs = bench.build(cuda_device, 256)
-    tr = bench.Trainer(layers, 1)
+    # three segments, as bench.py runs at world > 1: three graphs, each ending in its own flush of the
+    # packed epilogues (the exchange between them is a no-op in one process)
+    tr = bench.Trainer(layers, 1, segments=3)
     tr.compute(xs, gs)  # the first (initialising) step, eager, as bench.py's warm-up
     tr.flat.zero_()
     tr.capture(xs, gs)
     tr.flat.zero_()
-    tr.graph.replay()
+    for g in tr.graphs:
+        g.replay()
     torch.cuda.synchronize()
     grads = {n: [p.grad.detach().cpu().numpy().copy() for p in m.parameters()] for n, m in zip(names, layers)}
 
@@ -62,11 +65,8 @@ def test_bench_graph_composition_vs_oracle(cuda_device, monkeypatch):
         gw_ref = om.weight.grad.numpy()
         assert rel_err(mine["weight"], gw_ref, aw.reshape(gw_ref.shape)) < 1e-5, (name, "grad_w")
         ga, gr = mine["alpha_cim"], om.alpha_cim.grad.numpy()
-        a = om.alpha_cim.detach().numpy()
-        inner = (a != a.max()) & (a != a.min())
-        aa = np.broadcast_to(aa, gr.shape)
-        assert rel_err(ga[inner], gr[inner], aa[inner]) < 1e-5, (name, "grad_alpha_cim")
-        assert np.abs(ga - gr).max() <= 1e-5 * np.abs(gr).max(), (name, "grad_alpha_cim (max / min entries)")
+        # every entry; the max / min ones with the exact terms of the alpha quantiser's scale gradient
+        assert rel_err(ga, gr, alpha_cim_terms(om.alpha_cim.detach().numpy(), aa)) < 1e-5, (name, "grad_alpha_cim")
         d = om.dbg
         qn_a, qp_a = co.lsq_act_params(bits)  # unsigned even for the signed first layer (lsq.py:537-538)
         qn_w, qp_w = co.lsq_weight_params(bits)

@@ -8,17 +8,19 @@ module, lsq.py:511-588), and the layers outside the shift fast path.
   whole batch (the batch-summed gradients included), elementwise, plus run-to-run bit identity.
 * ResNet-56's first conv, forced to w8a8 by ReplaceModuleTool (utils/wrapper/replace_module.py:83-95):
   3 -> 16 @ 32, signed input, xbar 64 (K = 27, T = 1, 64 slice pairs, the int8-wrapped binary_mask),
-  at B = 2 and B = 256.  It is off the shift fast path (which takes 2 or 3 equal slices): the general
-  recompute kernels, deterministic (fixed-order reductions, no atomics).
+  at B = 2 and B = 256.  Since round 4 it runs the shift fast path's w8a8 form (cim_fwd_v3_kernel<8,1,8,1>
+  with plane state, the v7 backward pair and shift_stats8_kernel; test_abi_host.py asserts the routing);
+  a w8a8 shape that fast path refuses (C = 8, K = 72) keeps the general recompute kernels under test.
+  Deterministic (fixed-order reductions, no atomics).
 * alpha only (adc_shift=False) at B = 256: the 32x32 stage, a stride-2 transition and the 8x8 stage.
 * Shift layers the fast path refuses for other reasons: 128 output channels (more than four 16-channel
   blocks) and a batch-1 8x8 image (M % 128 != 0).
 
 Bars (north_star 1e-5): out within 1e-6 and grad_x / grad_w / grad_beta within 1e-5 of
 max(|ref|, sum of |terms|) element by element (the oracle's fp64 re-run on |operands|); grad_alpha_cim
-elementwise 1e-5 of its terms, the max / min entries of alpha_cim -- which collect the alpha quantiser's
-scale gradient from every element -- 1e-5 of the terms of that sum too; the step sizes within 1e-5 of
-their sum of |terms|.
+elementwise 1e-5 of its terms (conftest.alpha_cim_terms: for the max / min entries of alpha_cim, which
+collect the alpha quantiser's scale gradient from every element, the exact terms of that sum too); the
+step sizes within 1e-5 of their sum of |terms|.
 """
 import math
 
@@ -26,7 +28,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import rel_err
+from conftest import alpha_cim_terms, rel_err
 from oracle import cim_module_oracle as cmo
 from oracle import cim_oracle as co
 
@@ -137,20 +139,9 @@ def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True, shi
     if shift:
         assert rel_err(np_(r1["gb"]), np_(om.beta_cim.grad), terms[3].reshape(om.beta_cim.shape)) < 1e-5, "grad_beta"
     ga, gr = np_(r1["ga"]), np_(om.alpha_cim.grad)
-    a = np_(om.alpha_cim)
-    inner = (a != a.max()) & (a != a.min())
-    aab = np.broadcast_to(aa, gr.shape)
-    assert rel_err(ga[inner], gr[inner], aab[inner]) < 1e-5, "grad_alpha_cim"
-    # the max / min entries also collect the alpha quantiser's scale gradient (lsq.py:566-571: scale =
-    # (max - min) / 254, alpha_q = round_pass(alpha / scale).clamp(1, 255) * scale): a sum over every entry
-    # of d loss / d alpha_q_e * (rp_e - alpha_e / scale) / 254, whose |terms| bound those two entries
-    a64 = a.astype(np.float64)
-    sc = (a64.max() - a64.min()) / 254.0
-    rp = np.clip(np.rint(a64 / sc), 1, 255)
-    edge_terms = ((aab + np.abs(gr)) * (rp + np.abs(a64 / sc))).sum() / 254.0
-    edge = ~inner
-    assert np.all(np.abs(ga - gr)[edge] <= 1e-5 * (aab[edge] + np.abs(gr[edge]) + edge_terms)), \
-        "grad_alpha_cim (max / min entries)"
+    # every entry, the max / min ones included: those also collect the alpha quantiser's scale gradient
+    # (lsq.py:566-571), a sum over every entry whose exact |terms| alpha_cim_terms adds
+    assert rel_err(ga, gr, alpha_cim_terms(np_(om.alpha_cim), aa)) < 1e-5, "grad_alpha_cim"
     d = om.dbg
     t_act = _scalar_terms(x, np_(d["x_q"].grad), d["sa"].item(), 0, qp_a, 1.0 / math.sqrt(x.size * qp_a))
     t_w = _scalar_terms(w, np_(d["w_q"].grad), d["sw"].item(), qn_w, qp_w, 1.0 / math.sqrt(w.size * qp_w))
@@ -178,8 +169,16 @@ def test_resnet56_shift_fullbatch_vs_oracle(cuda_device, monkeypatch, C, O, H, s
 @pytest.mark.parametrize("B", [2, 256])
 def test_resnet56_conv1_w8a8_shift_vs_oracle(cuda_device, monkeypatch, B):
     """ResNet-56's first conv under the scale/shift ADC: w8a8 (replace_module.py:83-95), signed input,
-    3 -> 16 @ 32, xbar 64 -- the general kernels, bit-identical run to run."""
+    3 -> 16 @ 32, xbar 64 -- the shift fast path's w8a8 form (v3<8,1,8,1> + v7 + shift_stats8_kernel),
+    bit-identical run to run."""
     _check(cuda_device, monkeypatch, 3, 16, 32, 1, 8, B, 9200 + B, signed=True)
+
+
+def test_w8a8_shift_general_kernels_vs_oracle(cuda_device, monkeypatch):
+    """A w8a8 signed shift layer the fast path refuses (C = 8 -> K = 72 > xbar 64: two tiles; test_abi_host
+    shows cimq_module_shift_supported returns 0 for it): the general recompute kernels at w8a8 with signed
+    input and the int8-wrapped mask, against the module oracle on the whole batch."""
+    _check(cuda_device, monkeypatch, 8, 16, 16, 1, 8, 8, 9250, signed=True)
 
 
 @pytest.mark.parametrize("C,O,H,s,B", [(16, 128, 8, 1, 2), (16, 16, 8, 1, 1), (32, 32, 8, 2, 1)])

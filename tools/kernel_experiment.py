@@ -33,6 +33,14 @@ VARIANTS = {
     "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],
     "fwd_nostagex": ["CIMQ_EXP_FWD_NOSTAGEX"],
     "fwd_nostage": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX"],
+    # round 5: the compute phase of the forward -- without the LDS gather / the ADC and state bits /
+    # the state bits only, and the staging-free skeletons
+    "fwd_nogather": ["CIMQ_EXP_FWD_NOGATHER"],
+    "fwd_noadc": ["CIMQ_EXP_FWD_NOADC"],
+    "fwd_nostate": ["CIMQ_EXP_FWD_NOSTATE"],
+    "fwd_ns_ng": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX", "CIMQ_EXP_FWD_NOGATHER"],
+    "fwd_ns_ng_na": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX", "CIMQ_EXP_FWD_NOGATHER", "CIMQ_EXP_FWD_NOADC"],
+    "fwd_ns_nst": ["CIMQ_EXP_FWD_NOSTAGEW", "CIMQ_EXP_FWD_NOSTAGEX", "CIMQ_EXP_FWD_NOSTATE"],
     # the module epilogue's grad_w role: without the weight quantiser's loads / stores, without the
     # slab sums (tools/tail_sweep.sh with CIMQ_LIB_PATH=<variant lib>)
     "tail_noepi": ["CIMQ_EXP_TAIL_NOEPI"],
