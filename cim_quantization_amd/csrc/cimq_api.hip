@@ -531,8 +531,12 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
   a.nwg = p7.ok ? 0 : g.T * g.FBT * g.NKS * 64;       // general / dense grad_x operand
   a.ncpbt = p7.ok ? p7.v.NCPBT : 1;
   a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;  // v8 grad_x operand
+  const Plan5 p5 = f5_plan(g);
+  a.wf5 = reinterpret_cast<v4i*>(wr + L.wf5);
+  a.f5 = p5.v;
+  a.nw5 = (int)f5_frag_items(g, p5);  // cim_fwd5_kernel's weight operand
   a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.npp, 256), 1024));
+  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.npp, 256), 1024));
   return a;
 }
 
@@ -577,7 +581,7 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
     if (beta_cim) {  // the shift ADC: beta into the thresholds, and the per-channel beta sums
       a.beta = beta_cim;
       a.npp += g.Opad;
-      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.npp, 256), 1024));
+      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.npp, 256), 1024));
     }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     if (fwd_actq_ok(g)) a.nact_blocks = 0;  // the forward's row staging quantises (stage_rows_q)

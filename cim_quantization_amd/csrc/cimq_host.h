@@ -15,6 +15,7 @@
 
 #include "../../include/cimq.h"
 #include "cimq_c1.hip"
+#include "cimq_fwd5.hip"
 
 
 namespace cimq {
@@ -154,17 +155,20 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wf5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
 };
+
+inline size_t f5_frag_bytes(const Geo& g);  // after f5_plan
 
 inline CtxLayout ctx_layout(const Geo& g) {
   CtxLayout L;
   size_t o = 0;
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
+  L.wf5 = o; o = align256(o + f5_frag_bytes(g));  // cim_fwd5_kernel's weight operand
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
   L.wcy = o; o = align256(o + (size_t)g.T * 12 * g.NKS * 64 * 16);  // v8 grad_x operand (<= 12 blocks / tile)
   L.thi = o; o = align256(o + npar * 4);
@@ -687,6 +691,55 @@ inline bool fwd_actq_ok(const Geo& g) {
          g.P % 64 == 0 && g.lsq_qp >= 0.f && g.lsq_qp < 255.f && v3_plan(g).ok && v7_bwd(g) && !c1_plan(g).ok;
 }
 
+// ---- the w3a3 forward on the slice-planar patch (cimq_fwd5.hip) ----
+struct Plan5 {
+  bool ok;
+  F5 v;
+  size_t lds;
+  int cb;  // 16-channel input blocks (the kernel's template argument)
+};
+
+inline Plan5 f5_plan(const Geo& g) {
+  Plan5 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("FWD5", 1) == 0) return p;
+  // the module forward with the fused activation quantiser, w3a3 1-bit slices, the ternary library ADC,
+  // 3x3 / pad 1 / stride 1 or 2, 16 or 32 input channels, whole 16-pixel row groups, 128-pixel m-tiles
+  // inside one image
+  if (!fwd_actq_ok(g) || g.mode != ADC_TERNARY || g.variant != VAR_LIBRARY) return p;
+  if (g.nbw != 3 || g.nba != 3 || g.bsw != 1 || g.bsa != 1) return p;
+  if (g.KH != 3 || g.KW != 3 || g.PH != 1 || g.PW != 1 || g.SH != g.SW || (g.SH != 1 && g.SH != 2)) return p;
+  if (g.C % 16 != 0 || g.C / 16 > 2 || g.O % 16 != 0 || g.Wo % 16 != 0 || g.P % 128 != 0) return p;
+  if (g.W % 4 != 0 || g.T > 8) return p;
+  F5& v = p.v;
+  v.lwo = 0;
+  while ((1 << v.lwo) < g.Wo) ++v.lwo;
+  if ((1 << v.lwo) != g.Wo) return p;
+  v.R = 128 / g.Wo;
+  v.RH = (v.R - 1) * g.SH + 3;
+  v.WP = g.W + 2;
+  v.nmt = g.M / 128;
+  v.ntc = 0;
+  for (int i = 0; i < g.T; ++i) {
+    v.tc0[i] = v.ntc;
+    const int flo = i * g.xbar, fhi = std::min(flo + g.xbar, g.K);
+    const int cblo = (flo / 9) / 16, cbhi = ((fhi - 1) / 9) / 16;
+    for (int cb = cblo; cb <= cbhi; ++cb) {
+      if (v.ntc >= kF5MaxTc) return p;
+      v.tcb[v.ntc++] = cb;
+    }
+  }
+  v.tc0[g.T] = v.ntc;
+  p.cb = g.C / 16;
+  p.lds = (size_t)v.ntc * 9 * 1024 + (size_t)g.T * 9 * 16 * (16 + 4) + a16((size_t)2 * ((int)g.lsq_qp + 2) * 4) + 16 +
+          (size_t)v.RH * p.cb * v.WP * 48;
+  p.ok = p.lds <= (size_t)80 * 1024;  // two 512-thread blocks per CU
+  return p;
+}
+// wf5 fragments of a layer (all output-channel blocks)
+inline size_t f5_frag_items(const Geo& g, const Plan5& p) { return p.ok ? (size_t)g.OB16 * p.v.ntc * 9 * 64 : 0; }
+inline size_t f5_frag_bytes(const Geo& g) { return f5_frag_items(g, f5_plan(g)) * 16; }
+
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
   int rows, nchunks, nchunks_bwd;
@@ -841,6 +894,9 @@ inline void prof_end(int slot, hipStream_t s) {
 int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, int* ps_dbg,
                    float* adc_dbg, hipStream_t s,
                    const ActQ* aq = nullptr);
+// cimq_part_fwd5.hip: the w3a3 module forward on the slice-planar patch (f5_plan)
+int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
+                hipStream_t s, const ActQ* aq);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
 // shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words

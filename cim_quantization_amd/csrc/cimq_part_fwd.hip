@@ -48,6 +48,10 @@ int launch_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, flo
   CtxLayout L = ctx_layout(g);
   const Plan3 p = v3_plan(g);
   if (p.ok && !DBG) {
+    if (aq) {
+      const Plan5 p5 = f5_plan(g);
+      if (p5.ok) return launch_fwd5(g, p5, ctx, sw, sa, out, s, aq);
+    }
     if (g.KS == 1) return launch_fwd_v3<NBP, 1>(g, p, ctx, sw, sa, out, s, aq);
     return launch_fwd_v3<NBP, 2>(g, p, ctx, sw, sa, out, s, aq);
   }

@@ -1,0 +1,25 @@
+// cimq_part_fwd5.hip -- launch of the w3a3 module forward on the slice-planar patch (cimq_fwd5.hip,
+// lsq.py:141-233 with the activation quantiser of lsq.py:544-549).  Own translation unit of libcimq.so.
+#include "cimq_host.h"
+
+namespace cimq {
+
+int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
+                hipStream_t s, const ActQ* aq) {
+  if (!p.ok || !aq || !g.onchw) return fail(CIMQ_EINVAL, "internal: cim_fwd5 off its plan");
+  CtxLayout L = ctx_layout(g);
+  auto kern = p.cb == 1 ? cim_fwd5_kernel<1> : cim_fwd5_kernel<2>;
+  CIMQ_TRY(set_lds(kern, p.lds));
+  // two 512-thread blocks per CU (the kernel's occupancy: 4 waves per SIMD), a grid-stride walk over
+  // the 128-pixel m-tiles; the output-channel blocks in y
+  const int per_ob = std::max(1, tune("FWD5_GRID", 512) / g.OB16);
+  dim3 grid(std::min(p.v.nmt, per_ob), g.OB16);
+  const int slot = prof_begin(KID_FWD_V7, g, s);
+  hipLaunchKernelGGL(kern, grid, dim3(512), p.lds, s, g, p.v, reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wf5),
+                     params_of(g, ctx), sw, sa, aq->x, aq->signed_act, out,
+                     reinterpret_cast<uint32_t*>(ctx + L.st), reinterpret_cast<uint32_t*>(ctx + L.xhat));
+  prof_end(slot, s);
+  return check_hip("cim_fwd5");
+}
+
+}  // namespace cimq
