@@ -1,20 +1,22 @@
-// cimq_fwd5.hip -- the forward of the w3a3 module layers with 16 or 32 input channels (lsq.py:141-233,
-// the LSQ activation quantiser of lsq.py:544-549 fused in), rebuilt around one LDS layout that feeds the
-// int8 MFMA straight from ds_read_b128:
+// cimq_fwd5.hip -- the forward of the w3a3 module layers (lsq.py:141-233, the LSQ activation quantiser of
+// lsq.py:544-549 fused in), rebuilt around one LDS layout that feeds the int8 MFMA straight from
+// ds_read_b128:
 //
 //   * the activation patch of a 128-pixel m-tile is stored slice-planar and channel-innermost,
-//     [row][16-channel block][col][slice j][16 channels], so the 16 contraction values one lane of
-//     v_mfma_i32_16x16x64_i8 needs -- 16 channels at one kernel position (kh, kw) -- are 16 contiguous
+//     [image][row][16-channel block][col][slice j][16 channels], so the 16 contraction values one lane
+//     of v_mfma_i32_16x16x64_i8 needs -- 16 channels at one kernel position (kh, kw) -- are 16 contiguous
 //     bytes of one slice: one ds_read_b128 per (slice, K-step), no byte transposes, no index table;
 //   * the contraction of a crossbar tile is ordered (16-channel block, position p = kh*3 + kw) with the
 //     positions padded to 12 = 3 K-steps of 4 lane groups (lane group g4 of K-step s holds position
-//     4s + g4), so a lane's patch offset is one of three per-lane constants plus an immediate; the
+//     4s + g4), so a lane's patch offset is one of three per-lane constants plus a uniform offset; the
 //     weight side (wf5, built by the module prologue) is zero for every (channel, position) outside the
 //     tile and for the padding positions, which makes each tile's partial sums exactly the reference's
 //     (lsq.py:179-185: any order of a tile's rows gives the same integer sum);
-//   * 8 waves per block, one 16-pixel group each, two blocks per CU: the weight fragments of the
-//     block's 16 output channels and their ADC thresholds stay resident in LDS, a wave never waits for
-//     another except at the one barrier pair around the row staging of each m-tile.
+//   * 8 waves per block, one 16-pixel group each, two blocks per CU.  The crossbar tiles are processed
+//     in groups whose weight fragments and activation channels fit the block's LDS budget: with one
+//     group (16 / 32 input channels) the weight side is staged once and stays resident for all the
+//     block's m-tiles; with more (64 channels) each group's is staged per m-tile, the output still
+//     summed in registers across the groups.
 // Outputs are those of cim_fwd_v3_kernel<4, KS, 3, *>: out (NCHW), the compact state words of the v7
 // backward (bit 3*(k*3 + j) + {0 STE pass, 1 code != 0, 2 code < 0}), the backward ctx words of the rows
 // the m-tile owns; the ADC sum runs in the same order (tiles ascending, k and j descending), so out is
@@ -24,16 +26,24 @@
 
 namespace cimq {
 
-constexpr int kF5MaxTc = 8;  // (tile, channel-block) pairs: 2 for C = 16, 4 for C = 32 at xbar 128
+constexpr int kF5MaxTc = 8;   // (tile, channel-block) pairs: 2 / 4 / 8 for C = 16 / 32 / 64 at xbar 128
+constexpr int kF5MaxGrp = 4;  // tile groups
 
 // host-computed plan (cimq_host.h: f5_plan)
 struct F5 {
-  int lwo;               // log2(Wo)
-  int R, RH, WP;         // output rows per m-tile, patch rows (R-1)*SH + 3, patch row length W + 2
-  int nmt;               // M / 128
-  int ntc;               // (tile, channel-block) pairs
+  int lwo;                 // log2(Wo)
+  int IPM;                 // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
+  int R, RH, WP;           // output rows per image slot, patch rows (R-1)*SH + 3, patch row length W + 2
+  int NCBP;                // channel blocks one patch holds (the widest group's span)
+  int nmt;                 // M / 128
+  int ntc;                 // (tile, channel-block) pairs
+  int ngrp;                // tile groups
+  int tcmax;               // most pairs in one group
   unsigned char tc0[kF5MaxTc + 1];  // first pair of tile i (tc0[T] = ntc)
   unsigned char tcb[kF5MaxTc];      // channel block of pair t
+  unsigned char gt0[kF5MaxGrp + 1]; // first tile of group q (gt0[ngrp] = T)
+  unsigned char gcb0[kF5MaxGrp], gcb1[kF5MaxGrp];  // channel-block span of group q
+  unsigned char gown[kF5MaxGrp];    // first channel block whose ctx words group q writes
 };
 
 // the weight operand of one (ob, pair t, K-step s, w-slice k) fragment, lane l: output channel
@@ -71,23 +81,25 @@ __device__ inline void wf5_item(const Geo& g, const F5& v, const WS& ws, v4i* __
   wf5[t] = o;
 }
 
-// LDS byte offset of the patch element (row, cb, col), slice 0 (slice j at + 16 j)
-__device__ inline int f5_off(int CB, int WP, int row, int cb, int col) { return ((row * CB + cb) * WP + col) * 48; }
+// LDS byte offset of the patch element (row, channel-block slot, col) of one image slot, slice 0
+// (slice j at + 16 j)
+__device__ inline int f5_off(int NCB, int WP, int row, int cb, int col) { return ((row * NCB + cb) * WP + col) * 48; }
 
-template <int CB>
+#ifdef CIMQ_TU_FWD5  // non-template kernel: defined in its launcher's translation unit only
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void cim_fwd5_kernel(
     Geo g, F5 v, const v4i* __restrict__ wf5, Params pp, const float* __restrict__ sw_p,
     const float* __restrict__ sa_p, const float* __restrict__ x, const float* __restrict__ sgn_p,
     float* __restrict__ out, uint32_t* __restrict__ st, uint32_t* __restrict__ xcb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int ob = blockIdx.y;
-  const int nfr = v.ntc * 9;  // fragments of this block's output channels
-  v4i* bfr = reinterpret_cast<v4i*>(smem);                                   // [tc][s][k][64]
-  int4* prm = reinterpret_cast<int4*>(smem + (size_t)nfr * 1024);            // [i][j][k][16]
+  const int nfr = v.ntc * 9;  // this block's fragments ([pair][s][k], 64 lanes each)
+  v4i* bfr = reinterpret_cast<v4i*>(smem);                                   // [<= tcmax][s][k][64]
+  int4* prm = reinterpret_cast<int4*>(smem + (size_t)v.tcmax * 9 * 1024);    // [i][j][k][16] (all tiles)
   float* cfl = reinterpret_cast<float*>(prm + g.T * 9 * 16);                 // same order
   uint32_t* alut = reinterpret_cast<uint32_t*>(cfl + g.T * 9 * 16);          // [Qp + 2][fwd, bwd]
-  uint8_t* patch = reinterpret_cast<uint8_t*>(alut + 2 * ((int)g.lsq_qp + 2));  // [RH][CB][WP][3][16]
-  patch = reinterpret_cast<uint8_t*>(((uintptr_t)patch + 15) & ~(uintptr_t)15);
+  uint8_t* patch = reinterpret_cast<uint8_t*>(alut + 2 * ((int)g.lsq_qp + 2));
+  patch = reinterpret_cast<uint8_t*>(((uintptr_t)patch + 15) & ~(uintptr_t)15);  // [img][RH][NCBP][WP][3][16]
+  const int IMGB = v.RH * v.NCBP * v.WP * 48;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -95,8 +107,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   const bool literal = pp.flags[0] != 0;
   const bool sgn = *sgn_p != 0.f;
 
-  // the block's weight side, resident for all its m-tiles: fragments, thresholds, coefficients
-  batched_copy<4>(nfr * 64, bfr, [&](int idx) -> v4i { return wf5[(size_t)ob * nfr * 64 + idx]; });
+  // the weight fragments of group q (pairs tc0[gt0[q]] .. tc0[gt0[q+1]])
+  auto stage_b = [&](int q) {
+    const int a = v.tc0[v.gt0[q]], n = (v.tc0[v.gt0[q + 1]] - a) * 9 * 64;
+    const v4i* src = wf5 + ((size_t)ob * nfr + a * 9) * 64;
+    batched_copy<4>(n, bfr, [&](int idx) -> v4i { return src[idx]; });
+  };
+  // thresholds and coefficients of every tile (small): resident
   batched_copy<2>(g.T * 9 * 16, prm, [&](int idx) -> int4 {
     const int o = ob * 16 + (idx & 15), q = idx >> 4;  // q = i*9 + j*3 + k
     const int i = q / 9, jk = q - i * 9, j = jk / 3, k = jk - j * 3;
@@ -108,163 +125,175 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     const int i = q / 9, jk = q - i * 9, j = jk / 3, k = jk - j * 3;
     return literal ? 0.f : pp.coef[pidx(g, i, j, k, o)];
   });
+  if (v.ngrp == 1) stage_b(0);  // resident for all the block's m-tiles
   // padding columns 0 and WP-1 of every patch row: zero once (the staging writes data columns only)
-  for (int t = threadIdx.x; t < v.RH * CB * 2 * 12; t += blockDim.x) {
+  for (int t = threadIdx.x; t < v.IPM * v.RH * v.NCBP * 2 * 12; t += blockDim.x) {
     const int q = t % 12, rc = t / 12, side = rc & 1, rcb = rc >> 1;
     reinterpret_cast<uint32_t*>(patch + (rcb * v.WP + (side ? v.WP - 1 : 0)) * 48)[q] = 0u;
   }
   act_lut_build_q<3>(g, sa, sgn, alut);  // entries 0 .. Qp + 1 (NaN), then the block barrier
 
-  // this lane's A-operand pixel and its three position offsets (K-steps s = 0, 1, 2)
+  // this lane's A-operand pixel (image slot, output row / col) and its three position offsets
   const int Wo = 1 << v.lwo;
+  const int PI = g.P < 128 ? g.P : 128;  // pixels per image slot
   const int pl = wave * 16 + r16;
-  const int pix = f5_off(CB, v.WP, (pl >> v.lwo) * g.SH, 0, (pl & (Wo - 1)) * g.SW);
+  const int slot = pl / PI, pin = pl - slot * PI;
+  const int pix = slot * IMGB + f5_off(v.NCBP, v.WP, (pin >> v.lwo) * g.SH, 0, (pin & (Wo - 1)) * g.SW);
   int pat[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     const int p = min(4 * s + g4, 8);
     const int kh = p / 3, kw = p - kh * 3;
-    pat[s] = pix + f5_off(CB, v.WP, kh, 0, kw);
+    pat[s] = pix + f5_off(v.NCBP, v.WP, kh, 0, kw);
   }
   const int nan_e = (int)g.lsq_qp + 1;
-  const int QC = g.C >> 2;  // 4-channel groups
-  const int mt_px = 128;
-  const int tpi = g.P / mt_px;  // m-tiles per image
+  const int tpi = g.P >= 128 ? g.P / 128 : 1;  // m-tiles per image
+  const size_t HW = (size_t)g.H * g.W;
 
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
-    const int b = mt / tpi, p0 = (mt - b * tpi) * mt_px;
+    const int b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
+    const int p0 = g.P >= 128 ? (mt - b0 * tpi) * 128 : 0;
     const int oh0 = p0 >> v.lwo;
     const int ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
     // input rows whose ctx words this m-tile writes: its output rows' stride spans, to the image end
     // for its last m-tile (one output-channel block's blocks write them)
     const int own_lo = ob == 0 ? oh0 * g.SH : 0;
-    const int own_hi = ob == 0 ? (p0 + mt_px == g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
-    __syncthreads();  // the previous m-tile's waves are done with the patch
-    {
-      // row staging: item = (row, 4-channel group, col), col fastest (coalesced fp32 loads);
-      // quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices into the
-      // slice planes, store the ctx words of owned rows
-      const int n = v.RH * QC * g.W;
-      const size_t img = (size_t)b * g.C * g.H * g.W;
-      for (int base = threadIdx.x; base < n; base += 2 * (int)blockDim.x) {
-        float xv[2][4];
-        int meta[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int idx = base + u * (int)blockDim.x;
-          meta[u] = -1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
-          if (idx < n) {
-            const int col = idx % g.W, rq = idx / g.W;
-            const int q = rq % QC, row = rq / QC;
-            const int ih = ih0 + row;
-            meta[u] = idx;
-            if ((unsigned)ih < (unsigned)g.H) {
-              const float* src = x + img + ((size_t)(4 * q) * g.H + ih) * g.W + col;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) xv[u][e] = src[(size_t)e * g.H * g.W];
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (meta[u] < 0) continue;
-          const int idx = meta[u];
-          const int col = idx % g.W, rq = idx / g.W;
-          const int q = rq % QC, row = rq / QC;
-          const int ih = ih0 + row;
-          uint32_t* dst = reinterpret_cast<uint32_t*>(patch + f5_off(CB, v.WP, row, q >> 2, col + 1) + 4 * (q & 3));
-          if ((unsigned)ih >= (unsigned)g.H) {
-            dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
-            continue;
-          }
-          uint2 w[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = act_words_tab(xv[u][e], sa, g.lsq_qp, nan_e, alut);
-          uint32_t P[4];
-          tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
-          dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
-          if (ih >= own_lo && ih < own_hi) {
-            uint32_t* cb = xcb + img + ((size_t)(4 * q) * g.H + ih) * g.W + col;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) cb[(size_t)e * g.H * g.W] = w[e].y;
-          }
-        }
-      }
-    }
-    __syncthreads();
-
+    const int own_hi = ob == 0 ? (p0 + PI >= g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int m0 = mt * mt_px + wave * 16 + 4 * g4;  // output pixel of acc[0] (flattened b*P + p)
-    for (int i = 0; i < g.T; ++i) {
-      v4i ps[9];
+    const int m0 = mt * 128 + wave * 16 + 4 * g4;  // output pixel of acc[0] (flattened b*P + p)
+    for (int q = 0; q < v.ngrp; ++q) {
+      const int cb0 = v.gcb0[q], ncb = v.gcb1[q] - cb0 + 1;
+      const int QC = ncb * 4;  // staged 4-channel groups
+      __syncthreads();  // the previous group's / m-tile's waves are done with the patch (and the fragments)
+      if (v.ngrp > 1) stage_b(q);
+      {
+        // row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32
+        // loads); quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices
+        // into the slice planes, store the ctx words of owned rows and channel blocks
+        const int n = v.IPM * v.RH * QC * g.W;
+        for (int base = threadIdx.x; base < n; base += 2 * (int)blockDim.x) {
+          float xv[2][4];
+          int meta[2];
 #pragma unroll
-      for (int q = 0; q < 9; ++q) ps[q] = v4i{0, 0, 0, 0};
-      for (int tc = v.tc0[i]; tc < v.tc0[i + 1]; ++tc) {
-        const int cbo = v.tcb[tc] * v.WP * 48;
-        const v4i* bt = bfr + tc * 9 * 64 + lane;
+          for (int u = 0; u < 2; ++u) {
+            const int idx = base + u * (int)blockDim.x;
+            meta[u] = -1;
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const uint8_t* pa = patch + pat[s] + cbo;
-          v4i a[3], w[3];
+            for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
+            if (idx < n) {
+              const int col = idx % g.W, r1 = idx / g.W;
+              const int qq = r1 % QC, r2 = r1 / QC;
+              const int row = r2 % v.RH, sl = r2 / v.RH;
+              const int ih = ih0 + row;
+              meta[u] = idx;
+              if ((unsigned)ih < (unsigned)g.H) {
+                const float* src = x + ((size_t)(b0 + sl) * g.C + 4 * (cb0 * 4 + qq)) * HW + (size_t)ih * g.W + col;
 #pragma unroll
-          for (int j = 0; j < 3; ++j) a[j] = *reinterpret_cast<const v4i*>(pa + 16 * j);
-#pragma unroll
-          for (int k = 0; k < 3; ++k) w[k] = bt[(s * 3 + k) * 64];
-#pragma unroll
-          for (int k = 0; k < 3; ++k)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) ps[k * 3 + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], ps[k * 3 + j], 0, 0, 0);
-        }
-      }
-      // ADC + state bits of tile i: pairs kj = k*3 + j in descending order (bit 3*kj + {0,1,2} after
-      // the last shift), the output summed in cim_fwd_v3_kernel's order
-      uint32_t stw[4] = {0u, 0u, 0u, 0u};
-      if (!literal) {
-#pragma unroll
-        for (int k = 2; k >= 0; --k) {
-#pragma unroll
-          for (int j = 2; j >= 0; --j) {
-            const int pc = (i * 9 + j * 3 + k) * 16 + r16;
-            const int4 pv = prm[pc];
-            const float cf = cfl[pc];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int p = ps[k * 3 + j][r];
-              const uint64_t mhi = __builtin_amdgcn_ballot_w64(p >= pv.x);
-              const uint64_t mlo = __builtin_amdgcn_ballot_w64(p <= pv.y);
-              const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(p - pv.z) <= (unsigned)pv.w);
-              acc[r] += adc3(cf, mhi, mlo);
-              stw[r] = shin(shin(shin(stw[r], mlo), mhi | mlo), mps);
+                for (int e = 0; e < 4; ++e) xv[u][e] = src[(size_t)e * HW];
+              }
             }
           }
-        }
-      } else {
-        // degenerate alpha_q / scales (the literal-ADC flag): the per-partial-sum chain, summed in
-        // cim_fwd_v3_kernel's literal order (k, then j, ascending)
-        const int o = min(ob * 16 + r16, g.Opad - 1);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+          for (int u = 0; u < 2; ++u) {
+            if (meta[u] < 0) continue;
+            const int idx = meta[u];
+            const int col = idx % g.W, r1 = idx / g.W;
+            const int qq = r1 % QC, r2 = r1 / QC;
+            const int row = r2 % v.RH, sl = r2 / v.RH;
+            const int ih = ih0 + row;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(patch + sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) +
+                                                        4 * (qq & 3));
+            if ((unsigned)ih >= (unsigned)g.H) {
+              dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
+              continue;
+            }
+            uint2 w[4];
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const float al = pp.alpha[pidx(g, i, j, k, o)];
-            const float mk = pp.ckj[k * 3 + j];
+            for (int e = 0; e < 4; ++e) w[e] = act_words_tab(xv[u][e], sa, g.lsq_qp, nan_e, alut);
+            uint32_t P[4];
+            tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
+            dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
+            if (ih >= own_lo && ih < own_hi && cb0 + (qq >> 2) >= v.gown[q]) {
+              uint32_t* cbw = xcb + ((size_t)(b0 + sl) * g.C + 4 * (cb0 * 4 + qq)) * HW + (size_t)ih * g.W + col;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              acc[r] += adc_literal_sum(ps[k * 3 + j], g.mode, sw, sa, al, g.qn, g.qp, mk, r);
-              const bool pass = ste_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f;
-              const float code = code_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo);
-              stw[r] |= st_bits(pass, code) << (3 * (k * 3 + j));
+              for (int e = 0; e < 4; ++e) cbw[(size_t)e * HW] = w[e].y;
             }
           }
         }
       }
-      const int o = ob * 16 + r16;
-      if (o < g.O) {
-        uint32_t* s32 = st + ((size_t)i * g.M + m0) * g.O + o;
+      __syncthreads();
+
+      const int tbase = v.tc0[v.gt0[q]];  // first pair of the group (its fragments start bfr)
+      for (int i = v.gt0[q]; i < v.gt0[q + 1]; ++i) {
+        v4i ps[9];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stw[r];
+        for (int z = 0; z < 9; ++z) ps[z] = v4i{0, 0, 0, 0};
+        for (int tc = v.tc0[i]; tc < v.tc0[i + 1]; ++tc) {
+          const int cbo = (v.tcb[tc] - cb0) * v.WP * 48;
+          const v4i* bt = bfr + (tc - tbase) * 9 * 64 + lane;
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            const uint8_t* pa = patch + pat[s] + cbo;
+            v4i a[3], w[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a[j] = *reinterpret_cast<const v4i*>(pa + 16 * j);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) w[k] = bt[(s * 3 + k) * 64];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+              for (int j = 0; j < 3; ++j)
+                ps[k * 3 + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], ps[k * 3 + j], 0, 0, 0);
+          }
+        }
+        // ADC + state bits of tile i: pairs kj = k*3 + j in descending order (bit 3*kj + {0,1,2} after
+        // the last shift), the output summed in cim_fwd_v3_kernel's order
+        uint32_t stw[4] = {0u, 0u, 0u, 0u};
+        if (!literal) {
+#pragma unroll
+          for (int k = 2; k >= 0; --k) {
+#pragma unroll
+            for (int j = 2; j >= 0; --j) {
+              const int pc = (i * 9 + j * 3 + k) * 16 + r16;
+              const int4 pv = prm[pc];
+              const float cf = cfl[pc];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int p = ps[k * 3 + j][r];
+                const uint64_t mhi = __builtin_amdgcn_ballot_w64(p >= pv.x);
+                const uint64_t mlo = __builtin_amdgcn_ballot_w64(p <= pv.y);
+                const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(p - pv.z) <= (unsigned)pv.w);
+                acc[r] += adc3(cf, mhi, mlo);
+                stw[r] = shin(shin(shin(stw[r], mlo), mhi | mlo), mps);
+              }
+            }
+          }
+        } else {
+          // degenerate alpha_q / scales (the literal-ADC flag): the per-partial-sum chain, summed in
+          // cim_fwd_v3_kernel's literal order (k, then j, ascending)
+          const int o = min(ob * 16 + r16, g.Opad - 1);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const float al = pp.alpha[pidx(g, i, j, k, o)];
+              const float mk = pp.ckj[k * 3 + j];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                acc[r] += adc_literal_sum(ps[k * 3 + j], g.mode, sw, sa, al, g.qn, g.qp, mk, r);
+                const bool pass = ste_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f;
+                const float code = code_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo);
+                stw[r] |= st_bits(pass, code) << (3 * (k * 3 + j));
+              }
+            }
+          }
+        }
+        const int o = ob * 16 + r16;
+        if (o < g.O) {
+          uint32_t* s32 = st + ((size_t)i * g.M + m0) * g.O + o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stw[r];
+        }
       }
     }
     const int o = ob * 16 + r16;
@@ -274,5 +303,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     }
   }
 }
+#endif  // CIMQ_TU_FWD5
 
 }  // namespace cimq

@@ -696,7 +696,6 @@ struct Plan5 {
   bool ok;
   F5 v;
   size_t lds;
-  int cb;  // 16-channel input blocks (the kernel's template argument)
 };
 
 inline Plan5 f5_plan(const Geo& g) {
@@ -704,36 +703,62 @@ inline Plan5 f5_plan(const Geo& g) {
   memset(&p, 0, sizeof(p));
   if (tune("FWD5", 1) == 0) return p;
   // the module forward with the fused activation quantiser, w3a3 1-bit slices, the ternary library ADC,
-  // 3x3 / pad 1 / stride 1 or 2, 16 or 32 input channels, whole 16-pixel row groups, 128-pixel m-tiles
-  // inside one image
+  // 3x3 / pad 1 / stride 1 or 2, whole 16-pixel groups, 128-pixel m-tiles of R rows of one image or of
+  // 128 / P whole images
   if (!fwd_actq_ok(g) || g.mode != ADC_TERNARY || g.variant != VAR_LIBRARY) return p;
   if (g.nbw != 3 || g.nba != 3 || g.bsw != 1 || g.bsa != 1) return p;
   if (g.KH != 3 || g.KW != 3 || g.PH != 1 || g.PW != 1 || g.SH != g.SW || (g.SH != 1 && g.SH != 2)) return p;
-  if (g.C % 16 != 0 || g.C / 16 > 2 || g.O % 16 != 0 || g.Wo % 16 != 0 || g.P % 128 != 0) return p;
-  if (g.W % 4 != 0 || g.T > 8) return p;
+  if (g.C % 16 != 0 || g.O % 16 != 0 || g.W % 4 != 0 || g.P % 16 != 0) return p;
+  if (g.P >= 128 ? g.P % 128 != 0 : 128 % g.P != 0) return p;
+  if (g.Wo % 16 != 0 && 16 % g.Wo != 0) return p;
   F5& v = p.v;
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
   if ((1 << v.lwo) != g.Wo) return p;
-  v.R = 128 / g.Wo;
+  const int PI = std::min(g.P, 128);
+  v.IPM = 128 / PI;
+  v.R = PI / g.Wo;
   v.RH = (v.R - 1) * g.SH + 3;
   v.WP = g.W + 2;
   v.nmt = g.M / 128;
   v.ntc = 0;
   for (int i = 0; i < g.T; ++i) {
-    v.tc0[i] = v.ntc;
+    v.tc0[i] = (unsigned char)v.ntc;
     const int flo = i * g.xbar, fhi = std::min(flo + g.xbar, g.K);
     const int cblo = (flo / 9) / 16, cbhi = ((fhi - 1) / 9) / 16;
     for (int cb = cblo; cb <= cbhi; ++cb) {
       if (v.ntc >= kF5MaxTc) return p;
-      v.tcb[v.ntc++] = cb;
+      v.tcb[v.ntc++] = (unsigned char)cb;
     }
   }
-  v.tc0[g.T] = v.ntc;
-  p.cb = g.C / 16;
-  p.lds = (size_t)v.ntc * 9 * 1024 + (size_t)g.T * 9 * 16 * (16 + 4) + a16((size_t)2 * ((int)g.lsq_qp + 2) * 4) + 16 +
-          (size_t)v.RH * p.cb * v.WP * 48;
-  p.ok = p.lds <= (size_t)80 * 1024;  // two 512-thread blocks per CU
+  v.tc0[g.T] = (unsigned char)v.ntc;
+  // tile groups: greedy, while the block's LDS (the widest group's fragments and channel span) fits
+  // two blocks per CU
+  const size_t fixed = (size_t)g.T * 9 * 16 * (16 + 4) + a16((size_t)2 * ((int)g.lsq_qp + 2) * 4) + 16;
+  const size_t budget = (size_t)tune("FWD5_LDS_KB", 80) * 1024;
+  auto need = [&](int tcm, int ncb) { return fixed + (size_t)tcm * 9 * 1024 + (size_t)v.IPM * v.RH * ncb * v.WP * 48; };
+  v.ngrp = 0;
+  v.tcmax = 0;
+  v.NCBP = 0;
+  for (int i = 0; i < g.T;) {
+    if (v.ngrp >= kF5MaxGrp) return p;
+    int e = i + 1;
+    auto span = [&](int a, int b) { return v.tcb[v.tc0[b] - 1] - v.tcb[v.tc0[a]] + 1; };
+    auto pairs = [&](int a, int b) { return v.tc0[b] - v.tc0[a]; };
+    if (need(std::max(v.tcmax, pairs(i, e)), std::max(v.NCBP, span(i, e))) > budget) return p;
+    while (e < g.T && need(std::max(v.tcmax, pairs(i, e + 1)), std::max(v.NCBP, span(i, e + 1))) <= budget) ++e;
+    const int q = v.ngrp++;
+    v.gt0[q] = (unsigned char)i;
+    v.gcb0[q] = v.tcb[v.tc0[i]];
+    v.gcb1[q] = v.tcb[v.tc0[e] - 1];
+    v.gown[q] = (unsigned char)(q == 0 ? v.gcb0[0] : v.gcb1[q - 1] + 1);
+    v.tcmax = std::max(v.tcmax, pairs(i, e));
+    v.NCBP = std::max(v.NCBP, span(i, e));
+    i = e;
+  }
+  v.gt0[v.ngrp] = (unsigned char)g.T;
+  p.lds = need(v.tcmax, v.NCBP);
+  p.ok = p.lds <= budget;
   return p;
 }
 // wf5 fragments of a layer (all output-channel blocks)

@@ -1,5 +1,6 @@
 // cimq_part_fwd5.hip -- launch of the w3a3 module forward on the slice-planar patch (cimq_fwd5.hip,
 // lsq.py:141-233 with the activation quantiser of lsq.py:544-549).  Own translation unit of libcimq.so.
+#define CIMQ_TU_FWD5
 #include "cimq_host.h"
 
 namespace cimq {
@@ -8,7 +9,7 @@ int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, con
                 hipStream_t s, const ActQ* aq) {
   if (!p.ok || !aq || !g.onchw) return fail(CIMQ_EINVAL, "internal: cim_fwd5 off its plan");
   CtxLayout L = ctx_layout(g);
-  auto kern = p.cb == 1 ? cim_fwd5_kernel<1> : cim_fwd5_kernel<2>;
+  auto kern = cim_fwd5_kernel;
   CIMQ_TRY(set_lds(kern, p.lds));
   // two 512-thread blocks per CU (the kernel's occupancy: 4 waves per SIMD), a grid-stride walk over
   // the 128-pixel m-tiles; the output-channel blocks in y
