@@ -1,0 +1,235 @@
+// cimq_gw5.hip -- grad_w and the grad_alpha_cim partials of the w3a3 stride-1 module layers with 16 or 32
+// input channels (lsq.py:321-356), from the forward's compact state words (cimq_v7.hip) and ctx words:
+//
+//   gw[f, o]  = sum_j sum_m xhat_j[m, f] * g[m, o] * D_j[m, o],   D_j = sum_k cD_kj * pass_ijk  (i = tile of f)
+//   ga[i, kj, o] = sum_m code_ijk[m, o] * g[m, o]
+//
+// as one v_mfma_f32_16x16x32_bf16 contraction over (pixel, slice) per 16 weight rows f:
+//   * K is ordered (pixel pair, slot) with slots (j = 0, 1, 2, pad): one lane of the A operand holds the
+//     three ctx slices of two pixels of its row f, one lane of the B operand g * D_j of the same two
+//     pixels for its output channel, split hi / mid / lo (three MFMAs, fp32-accurate products: xhat is a
+//     small integer);
+//   * the block's input rows are staged once per 128-pixel m-tile into an "A-ready" LDS patch: per
+//     element the four bf16 (xhat_0, xhat_1, xhat_2, 0), so an A fragment is two ds_read_b64 at a lane
+//     offset fixed per 16-row block -- no per-element conversion in the MFMA loop;
+//   * block = (pixel chunk, 16-channel input block, 16-channel output block), as cim_bwd_gw_v7_kernel
+//     splits its pairs: the block's 144 weight rows are 9 16-row blocks in at most two tiles, its patch
+//     holds 16 channels; wave = 16 pixels of the m-tile, building the B operands of its own pixels and
+//     keeping its grad_w / grad_alpha sums in registers across the block's m-tiles.  At the end the 8
+//     waves are summed in LDS in wave order and the block writes its part of the chunk's slab (the
+//     module epilogue sums the slabs in chunk order: deterministic).
+#pragma once
+#include "cimq_v7.hip"
+
+namespace cimq {
+
+struct G5 {
+  int lwo;     // log2(Wo)
+  int R, RH, WP;  // output rows per m-tile, staged input rows R + 2, patch row length W + 2
+  int nmt;     // M / 128
+  int nst;     // m-tiles per block (chunk)
+  int nchunks; // blocks = slab chunks
+};
+
+#ifdef CIMQ_TU_GW5
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
+                        const float* __restrict__ gout, float* __restrict__ gw_slab, float* __restrict__ ga_slab) {
+  // block = (pixel chunk, input-channel block cb, output block ob): the 9 16-row blocks of rows
+  // f = 144 cb .. 144 cb + 143 (the 16 channels of cb at every (kh, kw)), which touch at most two tiles
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint2* pat = reinterpret_cast<uint2*>(smem);  // [16 channels][RH][WP] of (xhat_0 | xhat_1 << 16, xhat_2)
+  float* cdl = reinterpret_cast<float*>(smem + (size_t)16 * v.RH * v.WP * 8);  // cD_kj
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int cb = blockIdx.y / g.OB16, ob = blockIdx.y - cb * g.OB16;
+  const int o = ob * 16 + r16;
+  const int i_lo = (144 * cb) / 128, i_hi = (144 * cb + 143) / 128;  // tiles of the block's rows (xbar 128)
+  const int ntl = i_hi - i_lo + 1;
+  for (int t = threadIdx.x; t < 9; t += blockDim.x) cdl[t] = pp.ckj[18 + t];
+  // padding columns 0 and WP-1: zero once
+  for (int t = threadIdx.x; t < 16 * v.RH * 2; t += blockDim.x) {
+    const int side = t & 1, cr = t >> 1;
+    pat[cr * v.WP + (side ? v.WP - 1 : 0)] = make_uint2(0u, 0u);
+  }
+  __syncthreads();
+  // standard binary mask (cD_kj = 2^j): D_j = 2^j * popcount(pass bits of slice j); else the per-pair sum
+  const bool std_mask =
+      __builtin_amdgcn_ballot_w64(lane < 9 && cdl[lane < 9 ? lane : 0] != (float)(1 << (lane % 3))) == 0ull;
+  // grad_alpha of tile i belongs to the block of the channel block holding the tile's first row
+  // (as cim_bwd_gw_v7_kernel): each (tile, pair, channel) is summed by one block per chunk
+  bool own[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) own[q] = q < ntl && ((i_lo + q) * 128) / 144 == cb;
+
+  // per 16-row block fb: this lane's row f = 144 cb + 16 fb + r16 = (c, kh, kw) -> patch offset (uint2
+  // units, c relative to the block), and its tile (slot 0 or 1 of the block's tiles)
+  int aoff[9], atl[9];
+#pragma unroll
+  for (int fb = 0; fb < 9; ++fb) {
+    const int f = 16 * fb + r16, c = f / 9, p = f - 9 * c, kh = p / 3, kw = p - 3 * kh;
+    aoff[fb] = (c * v.RH + kh) * v.WP + kw;
+    atl[fb] = (144 * cb + 16 * fb) / 128 - i_lo;  // uniform
+  }
+  v4f acc[9];
+#pragma unroll
+  for (int fb = 0; fb < 9; ++fb) acc[fb] = v4f{0.f, 0.f, 0.f, 0.f};
+  float ga[2][9];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int kj = 0; kj < 9; ++kj) ga[q][kj] = 0.f;
+
+  const int Wo = 1 << v.lwo;
+  const int tpi = g.P / 128;
+  const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
+  for (int mt = mt_lo; mt < mt_hi; ++mt) {
+    const int b = mt / tpi, p0 = (mt - b * tpi) * 128;
+    const int oh0 = p0 >> v.lwo;
+    // this lane's four pixels p0 + 16 wave + 4 g4 .. +3: grad_out and the state words of the block's
+    // tiles, loaded ahead of the staging
+    const int pw = 16 * wave + 4 * g4;  // within the m-tile
+    const float4 gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pw);
+    uint32_t sq[2][4];
+    {
+      const size_t m = (size_t)b * g.P + p0 + pw;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sq[q][e] = q < ntl ? st[((size_t)(i_lo + q) * g.M + m + e) * g.O + o] : 0u;
+    }
+    __syncthreads();  // the previous m-tile's waves are done with the patch
+    {
+      // A-ready patch: input rows oh0 - 1 .. oh0 + R of the block's 16 channels; item = (c, row, col)
+      const int n = 16 * v.RH * g.W;
+      const uint32_t* src = xcb + ((size_t)b * g.C + 16 * cb) * g.H * g.W;
+      for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
+        uint32_t wv[4];
+        int dst[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = base + u * (int)blockDim.x;
+          dst[u] = -1;
+          wv[u] = 0u;
+          if (idx < n) {
+            const int col = idx % g.W, cr = idx / g.W, row = cr % v.RH, c = cr / v.RH;
+            const int ih = oh0 - 1 + row;
+            dst[u] = (c * v.RH + row) * v.WP + col + 1;
+            if ((unsigned)ih < (unsigned)g.H) wv[u] = src[((size_t)c * g.H + ih) * g.W + col];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (dst[u] < 0) continue;
+          // int8 ctx slices (lsq.py:160 truncation, wrapped) -> exact bf16 (the high half of the fp32)
+          const uint32_t f0 = __float_as_uint((float)(int8_t)(wv[u] & 0xFFu));
+          const uint32_t f1 = __float_as_uint((float)(int8_t)((wv[u] >> 8) & 0xFFu));
+          const uint32_t f2 = __float_as_uint((float)(int8_t)((wv[u] >> 16) & 0xFFu));
+          pat[dst[u]] = make_uint2(__builtin_amdgcn_perm(f1, f0, 0x07060302u), f2 >> 16);
+        }
+      }
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
+      const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
+      const int pin = pw + e0;
+      const int poff = (pin >> v.lwo) * v.WP + (pin & (Wo - 1));
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (q >= ntl) break;
+        const uint32_t s0 = sq[q][e0], s1 = sq[q][e0 + 1];
+        if (own[q]) {
+          // grad_alpha partials (lsq.py:321-333): code * g, the code the signed 2-bit field at bit 3kj + 1
+#pragma unroll
+          for (int kj = 0; kj < 9; ++kj) {
+            const int c0 = ((int)(s0 << (29 - 3 * kj))) >> 30, c1 = ((int)(s1 << (29 - 3 * kj))) >> 30;
+            ga[q][kj] = __builtin_fmaf((float)c1, gv1, __builtin_fmaf((float)c0, gv0, ga[q][kj]));
+          }
+        }
+        // B operand: g * D_j of the two pixels, slots (j = 0, 1, 2, 0), split hi / mid / lo
+        float d[8];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          float D0, D1;
+          if (std_mask) {
+            D0 = (float)(__popc(s0 & pass_mask_j(j, 3, 3)) << j);
+            D1 = (float)(__popc(s1 & pass_mask_j(j, 3, 3)) << j);
+          } else {
+            D0 = D1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const int bit = 3 * (k * 3 + j);
+              D0 += ((s0 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
+              D1 += ((s1 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
+            }
+          }
+          d[j] = gv0 * D0;
+          d[4 + j] = gv1 * D1;
+        }
+        d[3] = d[7] = 0.f;
+        v8bf bh, bm, bl;
+        split3x8(d, bh, bm, bl);
+#pragma unroll
+        for (int fb = 0; fb < 9; ++fb) {
+          if (atl[fb] != q) continue;  // uniform: the 16-row blocks of this tile
+          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + 1];
+          const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
+          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // the block's part of its chunk's slab: the 8 waves summed in LDS in wave order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [8 waves][64 lanes][4]
+  const size_t rows = (size_t)g.T * g.FBT * 16;
+  float* gws = gw_slab + (size_t)blockIdx.x * rows * g.Opad;
+#pragma unroll
+  for (int fb = 0; fb < 9; ++fb) {
+    reinterpret_cast<float4*>(red)[wave * 64 + lane] = make_float4(acc[fb][0], acc[fb][1], acc[fb][2], acc[fb][3]);
+    __syncthreads();
+    if (wave == 0) {  // lane holds rows 4 g4 + r of the block, column r16
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int w = 0; w < 8; ++w) {
+        const float4 q4 = reinterpret_cast<const float4*>(red)[w * 64 + lane];
+        t.x += q4.x; t.y += q4.y; t.z += q4.z; t.w += q4.w;
+      }
+      const int f0 = 144 * cb + 16 * fb + 4 * g4, i = f0 / g.xbar;
+      const size_t row0 = (size_t)i * g.FBT * 16 + (f0 - i * g.xbar);
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gws[(row0 + r) * g.Opad + o] = tv[r];
+    }
+    __syncthreads();
+  }
+  // grad_alpha of the owned tiles: the four lane groups, then the 8 waves
+  float* gas = ga_slab + (size_t)blockIdx.x * g.T * 9 * g.Opad;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (!own[q]) continue;  // uniform
+#pragma unroll
+    for (int kj = 0; kj < 9; ++kj) {
+      float t = ga[q][kj];
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      if (g4 == 0) red[(wave * 9 + kj) * 16 + r16] = t;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < 9 * 16) {
+      const int kj = threadIdx.x >> 4, oc = threadIdx.x & 15;
+      float t = 0.f;
+      for (int w = 0; w < 8; ++w) t += red[(w * 9 + kj) * 16 + oc];
+      gas[((size_t)(i_lo + q) * 9 + kj) * g.Opad + ob * 16 + oc] = t;
+    }
+    __syncthreads();
+  }
+}
+#endif  // CIMQ_TU_GW5
+
+}  // namespace cimq

@@ -16,6 +16,7 @@
 #include "../../include/cimq.h"
 #include "cimq_c1.hip"
 #include "cimq_fwd5.hip"
+#include "cimq_gw5.hip"
 
 
 namespace cimq {
@@ -765,6 +766,40 @@ inline Plan5 f5_plan(const Geo& g) {
 inline size_t f5_frag_items(const Geo& g, const Plan5& p) { return p.ok ? (size_t)g.OB16 * p.v.ntc * 9 * 64 : 0; }
 inline size_t f5_frag_bytes(const Geo& g) { return f5_frag_items(g, f5_plan(g)) * 16; }
 
+// ---- grad_w + grad_alpha partials of the w3a3 stride-1 16 / 32-channel layers (cimq_gw5.hip) ----
+struct PlanG5 {
+  bool ok;
+  G5 v;
+  size_t lds;
+  int pairs;  // (input, output) 16-channel block pairs: grid y
+};
+
+inline PlanG5 g5_plan(const Geo& g) {
+  PlanG5 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("GW5", 1) == 0) return p;
+  if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsa != 1) return p;
+  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
+  if (g.C % 16 != 0 || g.O % 16 != 0 || g.P % 128 != 0 || g.Wo % 4 != 0) return p;
+  if (g.T != (9 * g.C + 127) / 128 || !g.onchw) return p;
+  G5& v = p.v;
+  v.lwo = 0;
+  while ((1 << v.lwo) < g.Wo) ++v.lwo;
+  if ((1 << v.lwo) != g.Wo || 128 % g.Wo != 0) return p;
+  v.R = 128 / g.Wo;
+  v.RH = v.R + 2;
+  v.WP = g.W + 2;
+  v.nmt = g.M / 128;
+  p.pairs = (g.C / 16) * g.OB16;
+  // blocks: about two per CU; chunks (slabs) = blocks / pairs
+  const int want = std::max(1, tune("GW5_BLOCKS", 512) / p.pairs);
+  v.nst = std::max(1, (v.nmt + want - 1) / want);
+  v.nchunks = (v.nmt + v.nst - 1) / v.nst;
+  p.lds = std::max((size_t)16 * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64;
+  p.ok = p.lds <= (size_t)80 * 1024;
+  return p;
+}
+
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
   int rows, nchunks, nchunks_bwd;
@@ -785,7 +820,9 @@ inline WsLayout ws_layout(const Geo& g) {
   // statistics kernel does not take -- those run the general backward)
   const Plan7 p7 = v7_plan(g);
   const bool v7b = v7_bwd(g);
-  W.nchunks_bwd = (v9_plan(g).ok || c1_plan(g).ok) ? g.B : v7b ? p7.v.nchunks : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
+  const PlanG5 pg5 = g5_plan(g);
+  W.nchunks_bwd = (v9_plan(g).ok || c1_plan(g).ok) ? g.B : pg5.ok ? pg5.v.nchunks : v7b ? p7.v.nchunks
+                : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
   const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
@@ -922,6 +959,8 @@ int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa,
 // cimq_part_fwd5.hip: the w3a3 module forward on the slice-planar patch (f5_plan)
 int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
                 hipStream_t s, const ActQ* aq);
+// cimq_part_gw5.hip: grad_w + grad_alpha slabs of the w3a3 stride-1 16 / 32-channel layers (g5_plan)
+int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* gout, uint8_t* ws, hipStream_t s);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
 // shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words

@@ -36,6 +36,8 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
     CIMQ_TRY(check_hip("cim_bwd_gx_v8"));
   }
   if (parts & 2) {
+    const PlanG5 p5 = g5_plan(g);
+    if (p5.ok) return launch_gw5(g, p5, ctx, gout, ws, s);
     auto kern = g.SH == 1 ? cim_bwd_gw_v7_kernel<NBW, NBA, 1> : cim_bwd_gw_v7_kernel<NBW, NBA, 2>;
     CIMQ_TRY(set_lds(kern, p.lds_gw));
     const int slot = prof_begin(KID_GW_V7, g, s);
