@@ -25,7 +25,8 @@ namespace cimq {
 
 struct G5 {
   int lwo;     // log2(Wo)
-  int R, RH, WP;  // output rows per m-tile, staged input rows R + 2, patch row length W + 2
+  int IPM;     // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
+  int R, RH, WP;  // output rows per image slot, staged input rows R + 2, patch row length W + 2
   int nmt;     // M / 128
   int nst;     // m-tiles per block (chunk)
   int nchunks; // blocks = slab chunks
@@ -38,8 +39,9 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   // block = (pixel chunk, input-channel block cb, output block ob): the 9 16-row blocks of rows
   // f = 144 cb .. 144 cb + 143 (the 16 channels of cb at every (kh, kw)), which touch at most two tiles
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint2* pat = reinterpret_cast<uint2*>(smem);  // [16 channels][RH][WP] of (xhat_0 | xhat_1 << 16, xhat_2)
-  float* cdl = reinterpret_cast<float*>(smem + (size_t)16 * v.RH * v.WP * 8);  // cD_kj
+  uint2* pat = reinterpret_cast<uint2*>(smem);  // [16 channels][IPM][RH][WP] of (xhat_0 | xhat_1 << 16, xhat_2)
+  const int CH = v.IPM * v.RH;  // patch rows per channel
+  float* cdl = reinterpret_cast<float*>(smem + (size_t)16 * CH * v.WP * 8);  // cD_kj
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int cb = blockIdx.y / g.OB16, ob = blockIdx.y - cb * g.OB16;
@@ -48,7 +50,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int ntl = i_hi - i_lo + 1;
   for (int t = threadIdx.x; t < 9; t += blockDim.x) cdl[t] = pp.ckj[18 + t];
   // padding columns 0 and WP-1: zero once
-  for (int t = threadIdx.x; t < 16 * v.RH * 2; t += blockDim.x) {
+  for (int t = threadIdx.x; t < 16 * CH * 2; t += blockDim.x) {
     const int side = t & 1, cr = t >> 1;
     pat[cr * v.WP + (side ? v.WP - 1 : 0)] = make_uint2(0u, 0u);
   }
@@ -68,7 +70,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
   for (int fb = 0; fb < 9; ++fb) {
     const int f = 16 * fb + r16, c = f / 9, p = f - 9 * c, kh = p / 3, kw = p - 3 * kh;
-    aoff[fb] = (c * v.RH + kh) * v.WP + kw;
+    aoff[fb] = (c * CH + kh) * v.WP + kw;
     atl[fb] = (144 * cb + 16 * fb) / 128 - i_lo;  // uniform
   }
   v4f acc[9];
@@ -81,18 +83,22 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     for (int kj = 0; kj < 9; ++kj) ga[q][kj] = 0.f;
 
   const int Wo = 1 << v.lwo;
-  const int tpi = g.P / 128;
+  const int PI = g.P < 128 ? g.P : 128;  // pixels per image slot
+  const int tpi = g.P >= 128 ? g.P / 128 : 1;
   const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
   for (int mt = mt_lo; mt < mt_hi; ++mt) {
-    const int b = mt / tpi, p0 = (mt - b * tpi) * 128;
+    const int b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
+    const int p0 = g.P >= 128 ? (mt - b0 * tpi) * 128 : 0;
     const int oh0 = p0 >> v.lwo;
-    // this lane's four pixels p0 + 16 wave + 4 g4 .. +3: grad_out and the state words of the block's
-    // tiles, loaded ahead of the staging
+    // this lane's four pixels 16 wave + 4 g4 .. +3 of the m-tile (one image slot): grad_out and the state
+    // words of the block's tiles, loaded ahead of the staging
     const int pw = 16 * wave + 4 * g4;  // within the m-tile
-    const float4 gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pw);
+    const int sl = pw / PI, pin0 = pw - sl * PI;  // image slot, pixel within the slot
+    const int b = b0 + sl;
+    const float4 gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pin0);
     uint32_t sq[2][4];
     {
-      const size_t m = (size_t)b * g.P + p0 + pw;
+      const size_t m = (size_t)b * g.P + p0 + pin0;
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -100,9 +106,9 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     }
     __syncthreads();  // the previous m-tile's waves are done with the patch
     {
-      // A-ready patch: input rows oh0 - 1 .. oh0 + R of the block's 16 channels; item = (c, row, col)
-      const int n = 16 * v.RH * g.W;
-      const uint32_t* src = xcb + ((size_t)b * g.C + 16 * cb) * g.H * g.W;
+      // A-ready patch: input rows oh0 - 1 .. oh0 + R of each image slot, the block's 16 channels; item =
+      // (c, slot, row, col)
+      const int n = 16 * CH * g.W;
       for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
         uint32_t wv[4];
         int dst[4];
@@ -112,10 +118,11 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
           dst[u] = -1;
           wv[u] = 0u;
           if (idx < n) {
-            const int col = idx % g.W, cr = idx / g.W, row = cr % v.RH, c = cr / v.RH;
+            const int col = idx % g.W, cr = idx / g.W, row = cr % v.RH, c = cr / CH, slt = (cr / v.RH) - c * v.IPM;
             const int ih = oh0 - 1 + row;
-            dst[u] = (c * v.RH + row) * v.WP + col + 1;
-            if ((unsigned)ih < (unsigned)g.H) wv[u] = src[((size_t)c * g.H + ih) * g.W + col];
+            dst[u] = cr * v.WP + col + 1;
+            if ((unsigned)ih < (unsigned)g.H)
+              wv[u] = xcb[(((size_t)(b0 + slt) * g.C + 16 * cb + c) * g.H + ih) * g.W + col];
           }
         }
 #pragma unroll
@@ -135,8 +142,8 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     for (int s = 0; s < 2; ++s) {
       const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
       const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
-      const int pin = pw + e0;
-      const int poff = (pin >> v.lwo) * v.WP + (pin & (Wo - 1));
+      const int pin = pin0 + e0;  // within the image slot
+      const int poff = (sl * v.RH + (pin >> v.lwo)) * v.WP + (pin & (Wo - 1));
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (q >= ntl) break;

@@ -780,13 +780,15 @@ inline PlanG5 g5_plan(const Geo& g) {
   if (tune("GW5", 1) == 0) return p;
   if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsa != 1) return p;
   if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
-  if (g.C % 16 != 0 || g.O % 16 != 0 || g.P % 128 != 0 || g.Wo % 4 != 0) return p;
+  if (g.C % 16 != 0 || g.O % 16 != 0 || g.Wo % 4 != 0) return p;
+  if (g.P >= 128 ? g.P % 128 != 0 : (128 % g.P != 0 || g.P % 16 != 0)) return p;
   if (g.T != (9 * g.C + 127) / 128 || !g.onchw) return p;
   G5& v = p.v;
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
   if ((1 << v.lwo) != g.Wo || 128 % g.Wo != 0) return p;
-  v.R = 128 / g.Wo;
+  v.IPM = 128 / std::min(g.P, 128);
+  v.R = std::min(g.P, 128) / g.Wo;
   v.RH = v.R + 2;
   v.WP = g.W + 2;
   v.nmt = g.M / 128;
@@ -795,7 +797,7 @@ inline PlanG5 g5_plan(const Geo& g) {
   const int want = std::max(1, tune("GW5_BLOCKS", 512) / p.pairs);
   v.nst = std::max(1, (v.nmt + want - 1) / want);
   v.nchunks = (v.nmt + v.nst - 1) / v.nst;
-  p.lds = std::max((size_t)16 * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64;
+  p.lds = std::max((size_t)16 * v.IPM * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64;
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }
