@@ -93,12 +93,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int ob = blockIdx.y;
   const int nfr = v.ntc * 9;  // this block's fragments ([pair][s][k], 64 lanes each)
-  v4i* bfr = reinterpret_cast<v4i*>(smem);                                   // [<= tcmax][s][k][64]
+  // smem: weight fragments [<= tcmax][s][k][64] (v4i), then the tables below
   int4* prm = reinterpret_cast<int4*>(smem + (size_t)v.tcmax * 9 * 1024);    // [i][j][k][16] (all tiles)
   float* cfl = reinterpret_cast<float*>(prm + g.T * 9 * 16);                 // same order
   uint32_t* alut = reinterpret_cast<uint32_t*>(cfl + g.T * 9 * 16);          // [Qp + 2][fwd, bwd]
-  uint8_t* patch = reinterpret_cast<uint8_t*>(alut + 2 * ((int)g.lsq_qp + 2));
-  patch = reinterpret_cast<uint8_t*>(((uintptr_t)patch + 15) & ~(uintptr_t)15);  // [img][RH][NCBP][WP][3][16]
+  // [img][RH][NCBP][WP][3][16]: a 16-aligned byte offset from smem (an integer round trip through
+  // uintptr_t would turn the LDS pointer into a generic one: flat loads that wait on vmcnt too)
+  const size_t poff0 = (size_t)v.tcmax * 9 * 1024 + (size_t)g.T * 9 * 16 * (16 + 4) + (size_t)2 * ((int)g.lsq_qp + 2) * 4;
+  uint8_t* patch = smem + ((poff0 + 15) & ~(size_t)15);
   const int IMGB = v.RH * v.NCBP * v.WP * 48;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -111,7 +113,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   auto stage_b = [&](int q) {
     const int a = v.tc0[v.gt0[q]], n = (v.tc0[v.gt0[q + 1]] - a) * 9 * 64;
     const v4i* src = wf5 + ((size_t)ob * nfr + a * 9) * 64;
-    batched_copy<4>(n, bfr, [&](int idx) -> v4i { return src[idx]; });
+    batched_copy<4>(n, reinterpret_cast<v4i*>(smem), [&](int idx) -> v4i { return src[idx]; });
   };
   // thresholds and coefficients of every tile (small): resident
   batched_copy<2>(g.T * 9 * 16, prm, [&](int idx) -> int4 {
@@ -230,7 +232,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         for (int z = 0; z < 9; ++z) ps[z] = v4i{0, 0, 0, 0};
         for (int tc = v.tc0[i]; tc < v.tc0[i + 1]; ++tc) {
           const int cbo = (v.tcb[tc] - cb0) * v.WP * 48;
-          const v4i* bt = bfr + (tc - tbase) * 9 * 64 + lane;
+          const v4i* bt = reinterpret_cast<const v4i*>(smem) + (tc - tbase) * 9 * 64 + lane;  // LDS
 #pragma unroll
           for (int s = 0; s < 3; ++s) {
             const uint8_t* pa = patch + pat[s] + cbo;
