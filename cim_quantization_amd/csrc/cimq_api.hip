@@ -131,6 +131,8 @@ int launch_reduce_slab(const Geo& g, const uint8_t* ctx, uint8_t* ws, size_t sla
 int act_parts(const Geo& g) {
   if (v7_bwd(g)) {
     if (v9_plan(g).ok || c1_plan(g).ok) return g.B;
+    const PlanX5 p5 = x5_plan(g);
+    if (p5.ok) return p5.nblk;
     return g.B * v7_plan(g).v.nbands;
   }
   if (dense_plan(g) && g.input_kind == CIMQ_INPUT_RAW_LSQ && dense_lsq_parts(g) > 0) return dense_lsq_parts(g);
@@ -533,10 +535,12 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
   a.nwc = p7.ok ? g.T * p7.v.NCPBT * g.NKS * 64 : 0;  // v8 grad_x operand
   const Plan5 p5 = f5_plan(g);
   a.wf5 = reinterpret_cast<v4i*>(wr + L.wf5);
-  a.f5 = p5.v;
+  a.f5 = f5w_of(p5.v);
   a.nw5 = (int)f5_frag_items(g, p5);  // cim_fwd5_kernel's weight operand
+  a.wg5 = reinterpret_cast<v4i*>(wr + L.wg5);
+  a.nwx5 = (int)(x5_frag_bytes(g) / 16);  // cim_bwd_gx5_kernel's weight operand
   a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.npp, 256), 1024));
+  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.npp, 256), 1024));
   return a;
 }
 
@@ -581,7 +585,7 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
     if (beta_cim) {  // the shift ADC: beta into the thresholds, and the per-channel beta sums
       a.beta = beta_cim;
       a.npp += g.Opad;
-      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.npp, 256), 1024));
+      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.npp, 256), 1024));
     }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     if (fwd_actq_ok(g)) a.nact_blocks = 0;  // the forward's row staging quantises (stage_rows_q)

@@ -46,12 +46,26 @@ struct F5 {
   unsigned char gown[kF5MaxGrp];    // first channel block whose ctx words group q writes
 };
 
+// the part of the plan the weight prologue needs (kept small: it travels in every PrepJob)
+struct F5W {
+  int ntc;
+  unsigned char tc0[kF5MaxTc + 1];
+  unsigned char tcb[kF5MaxTc];
+};
+inline F5W f5w_of(const F5& v) {
+  F5W w;
+  w.ntc = v.ntc;
+  for (int i = 0; i <= kF5MaxTc; ++i) w.tc0[i] = v.tc0[i];
+  for (int i = 0; i < kF5MaxTc; ++i) w.tcb[i] = v.tcb[i];
+  return w;
+}
+
 // the weight operand of one (ob, pair t, K-step s, w-slice k) fragment, lane l: output channel
 // o = ob*16 + (l & 15), byte e = w-slice k of weight (c = cb*16 + e, position p = 4s + (l >> 4)),
 // rint(slice) as int8 as in wfrag_item; zero when p > 8 or the row f = c*9 + p is outside tile i
 // wf5[((ob*ntc + t)*3 + s)*3 + k][64]
 template <typename WS>
-__device__ inline void wf5_item(const Geo& g, const F5& v, const WS& ws, v4i* __restrict__ wf5, int t) {
+__device__ inline void wf5_item(const Geo& g, const F5W& v, const WS& ws, v4i* __restrict__ wf5, int t) {
   const int lane = t & 63;
   int r = t >> 6;
   const int k = r % 3;

@@ -1,0 +1,210 @@
+// cimq_gx5.hip -- grad_x of the w3a3 stride-1 module layers with 16 input and 16 output channels
+// (lsq.py:336-386 with the fused LSQ activation backward of lsq.py:549), from the forward's compact state
+// words (cimq_v7.hip), computed per INPUT pixel so that the nn.Fold adjoint is part of the contraction:
+//
+//   gx[c, ih, iw] = sw/nba * sum_i sum_{kh,kw} sum_{k,o} G_i[(ih+1-kh, iw+1-kw), (k, o)] * What_k[o, (c, kh, kw)]
+//   G_i[m, (k, o)] = g[m, o] * E_ik[m, o],   E_ik = sum_j cE_kj * pass_ijk   (tile i of row (c, kh, kw))
+//
+// on v_mfma_f32_16x16x32_bf16 (rows: 16 input pixels of one row; columns: the 16 channels; K: the 48 (k, o)
+// of one kernel position, two 32-deep steps), G split hi / mid / lo (fp32-accurate: What is a small
+// integer).  Per 128-input-pixel m-tile (4 input rows) and crossbar tile i the block builds G_i of the
+// six output rows those input rows read into an LDS "G patch" -- three bf16 planes [row][col][k][o] --
+// once; a wave then reads its A operand for kernel position (kh, kw) at the patch position shifted by
+// (kh, kw): one ds_read_b128 per plane and K-step, the shift an address offset.  The weight operand of
+// tile i (zero for the rows of other tiles) is staged per tile.  Every grad_x value is produced by one
+// lane, stored once after the LSQ backward: no fold pass, no ring, no atomics.
+#pragma once
+#include "cimq_v7.hip"
+
+namespace cimq {
+
+struct X5 {
+  int nmt;     // H / 4 * B: m-tiles of four input rows
+  int tpi;     // m-tiles per image
+};
+
+// weight operand of (tile i, position p, K-step s), lane l: channel c = l & 15, K values
+// kappa = 32 s + 8 (l >> 4) + e (e < 8) = (k, o) = (kappa / 16, kappa % 16), int8(slice_k) of weight
+// (o, f = 9 c + p) as bf16 (wcy_item's values), zero for kappa >= 48 or f outside tile i
+// wg5[((i * 9 + p) * 2 + s) * 64 + l]
+template <typename WS>
+__device__ inline void wg5_item(const Geo& g, const WS& ws, v4i* __restrict__ wg5, int t) {
+  const int lane = t & 63;
+  int r = t >> 6;
+  const int s = r & 1;
+  r >>= 1;
+  const int p = r % 9, i = r / 9;
+  const int c = lane & 15;
+  const int f = c * 9 + p;
+  const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
+  const bool ok = c < g.C && f >= flo && f < fhi;
+  uint32_t wd[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int kap = 32 * s + 8 * (lane >> 4) + e;
+    const int k = kap >> 4, o = kap & 15;
+    float val = 0.f;
+    if (ok && k < g.nbw) val = (float)to_i8_wrap(wslice(g, ws, f, k * g.Opad + o));
+    wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
+  }
+  v4i q;
+  q.x = (int)wd[0]; q.y = (int)wd[1]; q.z = (int)wd[2]; q.w = (int)wd[3];
+  wg5[t] = q;
+}
+
+#ifdef CIMQ_TU_GX5
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 8)))
+void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i* __restrict__ wg5, Params pp,
+                        const float* __restrict__ sw_p, const float* __restrict__ sa_p,
+                        const float* __restrict__ gout, const float* __restrict__ x, float* __restrict__ gx,
+                        float* __restrict__ gsa_part) {
+  // LDS: G patch, three planes [6 rows][W + 2 cols][48 (k, o)] bf16 (96 B per pixel; 32 B of slack after
+  // the last plane: the padded K-step reads past a pixel's 48 values), then the tile's weight operand
+  // [9 p][2 s][64 lanes] (16 B each), then the mask coefficients and the partials
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int WP = g.W + 2;
+  const int PLANE = 6 * WP * 96;                        // bytes per plane
+  const int OW5 = 3 * PLANE + 32;                       // weight operand offset
+  float* cel = reinterpret_cast<float*>(smem + OW5 + 18 * 1024);  // cE_kj
+  float* red = cel + 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const float sw = *sw_p, sa = *sa_p;
+  for (int t = threadIdx.x; t < 9; t += blockDim.x) cel[t] = pp.ckj[9 + t];
+  // zero padding columns 0 and W + 1 of every plane row (output columns -1 and W) and the slack after the
+  // last plane (read by the padded K-step of the last pixel, times a zero weight): written once
+  if (threadIdx.x < 2) reinterpret_cast<uint4*>(smem + 3 * PLANE)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+  for (int t = threadIdx.x; t < 3 * 6 * 2 * 6; t += blockDim.x) {
+    const int q = t % 6, rc = t / 6, side = rc & 1, pr = rc >> 1;  // pr = plane * 6 + row
+    reinterpret_cast<uint4*>(smem + (size_t)pr * WP * 96 + (side ? (WP - 1) * 96 : 0))[q] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  // standard mask (cE_kj = 2^k): E_k = 2^k * popcount(pass bits of slice k); else the per-pair sum
+  const bool std_mask =
+      __builtin_amdgcn_ballot_w64(lane < 9 && cel[lane < 9 ? lane : 0] != (float)(1 << (lane / 3))) == 0ull;
+  const float scale = sw / 3.f;
+  const float inv_sa = 1.f / sa;
+  float gpart = 0.f;
+  // this wave's 16 input pixels: row 4 mt + (wave >> 1), columns 16 (wave & 1) .. +15
+  const int rl = wave >> 1, iw0 = 16 * (wave & 1);
+
+  for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
+    const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
+    v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < g.T; ++i) {
+      __syncthreads();  // the previous tile's (or m-tile's) MFMAs are done with the patch and weights
+      // the tile's weight operand
+      batched_copy<2>(9 * 2 * 64, reinterpret_cast<v4i*>(smem + OW5),
+                      [&](int idx) -> v4i { return wg5[(size_t)i * 9 * 2 * 64 + idx]; });
+      // G patch of output rows r0 - 1 .. r0 + 4: item = (row, col, 4 channels), channels fastest
+      for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
+        const int oq = it & 3, rc = it >> 2, col = rc % g.W, row = rc / g.W;
+        const int oh = r0 - 1 + row;
+        float gv[4] = {0.f, 0.f, 0.f, 0.f};
+        uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
+        if ((unsigned)oh < (unsigned)g.Ho) {
+          const int pimg = oh * g.Wo + col;
+          const size_t m = (size_t)b * g.P + pimg;
+          s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + 4 * oq);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) gv[e] = gout[((size_t)b * g.O + 4 * oq + e) * g.P + pimg];
+        }
+        const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+        uint8_t* px = smem + (size_t)(row * WP + col + 1) * 96 + 8 * oq;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          float Gv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float E;
+            if (std_mask) {
+              E = (float)(__popc(sv[e] & pass_mask_k(k, 3)) << k);
+            } else {
+              E = 0.f;
+#pragma unroll
+              for (int j = 0; j < 3; ++j) E += ((sv[e] >> (3 * (k * 3 + j))) & 1u) ? cel[k * 3 + j] : 0.f;
+            }
+            Gv[e] = gv[e] * E;
+          }
+          // hi / mid / lo bf16 parts (split3x8's arithmetic on 4 values)
+          uint32_t ph[2], pm[2], plo[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t hb[2], mb[2], lb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const float vv = Gv[2 * h + u];
+              const __bf16 hh = (__bf16)vv;
+              const float r1 = vv - (float)hh;
+              const __bf16 mm = (__bf16)r1;
+              const float r2 = r1 - (float)mm;
+              const __bf16 ll = (__bf16)r2;
+              hb[u] = (uint32_t)__builtin_bit_cast(uint16_t, hh);
+              mb[u] = (uint32_t)__builtin_bit_cast(uint16_t, mm);
+              lb[u] = (uint32_t)__builtin_bit_cast(uint16_t, ll);
+            }
+            ph[h] = hb[0] | (hb[1] << 16);
+            pm[h] = mb[0] | (mb[1] << 16);
+            plo[h] = lb[0] | (lb[1] << 16);
+          }
+          *reinterpret_cast<uint2*>(px + 32 * k) = make_uint2(ph[0], ph[1]);
+          *reinterpret_cast<uint2*>(px + PLANE + 32 * k) = make_uint2(pm[0], pm[1]);
+          *reinterpret_cast<uint2*>(px + 2 * PLANE + 32 * k) = make_uint2(plo[0], plo[1]);
+        }
+      }
+      __syncthreads();
+      // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes
+      const v4i* wb = reinterpret_cast<const v4i*>(smem + OW5) + lane;
+#pragma unroll
+      for (int p = 0; p < 9; ++p) {
+        const int kh = p / 3, kw = p - 3 * kh;
+        // output pixel (oh, ow) = (ih + 1 - kh, iw + 1 - kw): patch row rl + 2 - kh, column iw + 2 - kw
+        const uint8_t* pa = smem + (size_t)((rl + 2 - kh) * WP + iw0 + r16 + 2 - kw) * 96 + 16 * g4;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const v8bf ah = as_v8bf(*reinterpret_cast<const v4i*>(pa + 64 * s));
+          const v8bf am = as_v8bf(*reinterpret_cast<const v4i*>(pa + PLANE + 64 * s));
+          const v8bf al = as_v8bf(*reinterpret_cast<const v4i*>(pa + 2 * PLANE + 64 * s));
+          const v8bf w = as_v8bf(wb[(p * 2 + s) * 64]);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, w, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w, acc, 0, 0, 0);
+        }
+      }
+    }
+    // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel r16: scale, LSQ activation backward, store
+    const int ih = r0 + rl, iw = iw0 + 4 * g4;
+    const size_t gi = (((size_t)b * g.C + r16) * g.H + ih) * g.W + iw;
+    const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
+    const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+    float o4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float gqv = acc[r] * scale;
+      // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v8_kernel
+      const float y1 = xv[r] / sa;
+      const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
+      const float rr2 = rintf(clv);
+      const float rp = (rr2 - clv) + clv;
+      const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
+      const float gy = pass ? gqv * sa : 0.f;
+      o4[r] = pass ? gqv : 0.f;
+      gpart += gqv * rp;
+      gpart += -(gy * (y1 * inv_sa));
+    }
+    *reinterpret_cast<float4*>(gx + gi) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+  }
+  // the block's d sa partial (fixed order: lanes, then waves)
+  for (int o = 32; o > 0; o >>= 1) gpart += __shfl_xor(gpart, o);
+  __syncthreads();
+  if (lane == 0) red[wave] = gpart;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 8; ++w) t += red[w];
+    gsa_part[blockIdx.x] = t;
+  }
+}
+#endif  // CIMQ_TU_GX5
+
+}  // namespace cimq

@@ -17,6 +17,7 @@
 #include "cimq_c1.hip"
 #include "cimq_fwd5.hip"
 #include "cimq_gw5.hip"
+#include "cimq_gx5.hip"
 
 
 namespace cimq {
@@ -156,13 +157,14 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wf5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
+  size_t xcode, xhat, wfrag, wf5, wg5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
 };
 
 inline size_t f5_frag_bytes(const Geo& g);  // after f5_plan
+inline size_t x5_frag_bytes(const Geo& g);  // after x5_plan
 
 inline CtxLayout ctx_layout(const Geo& g) {
   CtxLayout L;
@@ -170,6 +172,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wf5 = o; o = align256(o + f5_frag_bytes(g));  // cim_fwd5_kernel's weight operand
+  L.wg5 = o; o = align256(o + x5_frag_bytes(g));  // cim_bwd_gx5_kernel's weight operand
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
   L.wcy = o; o = align256(o + (size_t)g.T * 12 * g.NKS * 64 * 16);  // v8 grad_x operand (<= 12 blocks / tile)
   L.thi = o; o = align256(o + npar * 4);
@@ -802,6 +805,31 @@ inline PlanG5 g5_plan(const Geo& g) {
   return p;
 }
 
+// ---- grad_x of the w3a3 stride-1 16 -> 16-channel 32-wide layers, per input pixel (cimq_gx5.hip) ----
+struct PlanX5 {
+  bool ok;
+  X5 v;
+  size_t lds;
+  int nblk;  // grid = the d sa partials it leaves
+};
+
+inline PlanX5 x5_plan(const Geo& g) {
+  PlanX5 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("GX5", 1) == 0) return p;
+  if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsw != 1) return p;
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ || !g.onchw) return p;
+  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
+  if (g.C != 16 || g.O != 16 || g.W != 32 || g.H % 4 != 0 || g.Wo != g.W || g.Ho != g.H || g.T != 2) return p;
+  p.v.tpi = g.H / 4;
+  p.v.nmt = g.B * p.v.tpi;
+  p.nblk = std::min(p.v.nmt, tune("GX5_GRID", 512));
+  p.lds = (size_t)3 * 6 * (g.W + 2) * 96 + 32 + 18 * 1024 + 32 * 4;
+  p.ok = p.lds <= (size_t)80 * 1024;
+  return p;
+}
+inline size_t x5_frag_bytes(const Geo& g) { return x5_plan(g).ok ? (size_t)g.T * 9 * 2 * 64 * 16 : 0; }
+
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
   int rows, nchunks, nchunks_bwd;
@@ -961,6 +989,9 @@ int launch_fwd_any(const Geo& g, uint8_t* ctx, const float* sw, const float* sa,
 // cimq_part_fwd5.hip: the w3a3 module forward on the slice-planar patch (f5_plan)
 int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, const float* sa, float* out,
                 hipStream_t s, const ActQ* aq);
+// cimq_part_gx5.hip: grad_x (+ the fused act-LSQ backward) of the 16 -> 16-channel 32-wide layers (x5_plan)
+int launch_gx5(const Geo& g, const PlanX5& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
+               const float* x, float* gx, uint8_t* ws, hipStream_t s);
 // cimq_part_gw5.hip: grad_w + grad_alpha slabs of the w3a3 stride-1 16 / 32-channel layers (g5_plan)
 int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* gout, uint8_t* ws, hipStream_t s);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs

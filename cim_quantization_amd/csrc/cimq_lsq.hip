@@ -33,12 +33,13 @@ struct ModulePrep {
   v4i* wgx;   // general / dense grad_x operand (nwg == 0 on the v7 path)
   v4i* wcy;   // v8 grad_x operand (nwc == 0 unless the v7 backward applies)
   v4i* wf5;   // cim_fwd5_kernel's weight operand (nw5 == 0 unless f5_plan applies)
-  F5 f5;
+  F5W f5;
+  v4i* wg5;   // cim_bwd_gx5_kernel's weight operand (nwx5 == 0 unless x5_plan applies)
   int ncpbt;
   Params pp;
   float* scal;  // [0] sa, [1] sw, [2] alpha scale, [3] max(alpha_cim), [4] min(alpha_cim)
   int nact_blocks;
-  int nwf, nwg, nwc, npp, nw5;  // items of the weight-side roles
+  int nwf, nwg, nwc, npp, nw5, nwx5;  // items of the weight-side roles
   const float* amm;             // wide alpha_cim: [namm][2] per-block (max, min) of alpha_minmax_kernel
   int namm;                     // 0: every weight block reduces alpha_cim itself
 };
@@ -134,13 +135,14 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
       a.pp.flags[1] = a.pp.flags[2] = a.pp.flags[3] = 0;
     }
   }
-  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwc, e4 = e3 + a.nw5, total = e4 + a.npp;
+  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwc, e4 = e3 + a.nw5, e5 = e4 + a.nwx5, total = e5 + a.npp;
   for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
     if (t < e1) wfrag_item(g, ws, a.wfrag, t);
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wcy_item(g, ws, a.ncpbt, a.wcy, t - e2);
     else if (t < e4) wf5_item(g, a.f5, ws, a.wf5, t - e3);
-    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e4, a.beta);
+    else if (t < e5) wg5_item(g, ws, a.wg5, t - e4);
+    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e5, a.beta);
   }
 }
 

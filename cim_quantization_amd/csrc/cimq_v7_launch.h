@@ -16,7 +16,10 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   WsLayout W = ws_layout(g);
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
-  if (parts & 1) {
+  const PlanX5 px5 = x5_plan(g);
+  if ((parts & 1) && px5.ok && lsq) {
+    CIMQ_TRY(launch_gx5(g, px5, ctx, sw, sa, gout, x, gx, ws, s));
+  } else if (parts & 1) {
     const int np = p.v.NPART;
 #define CIMQ_GX8(L, S, N) cim_bwd_gx_v8_kernel<NBW, NBA, OBX, L, S, N>
 #ifdef CIMQ_TUNING
