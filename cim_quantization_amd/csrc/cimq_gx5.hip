@@ -1,18 +1,20 @@
-// cimq_gx5.hip -- grad_x of the w3a3 stride-1 module layers with 16 input and 16 output channels
-// (lsq.py:336-386 with the fused LSQ activation backward of lsq.py:549), from the forward's compact state
+// cimq_gx5.hip -- grad_x of the w3a3 stride-1 module layers 16 -> 16 channels at 32 x 32 and 32 -> 32 at
+// 16 x 16 (lsq.py:336-386 with the fused LSQ activation backward of lsq.py:549), from the forward's compact state
 // words (cimq_v7.hip), computed per INPUT pixel so that the nn.Fold adjoint is part of the contraction:
 //
 //   gx[c, ih, iw] = sw/nba * sum_i sum_{kh,kw} sum_{k,o} G_i[(ih+1-kh, iw+1-kw), (k, o)] * What_k[o, (c, kh, kw)]
 //   G_i[m, (k, o)] = g[m, o] * E_ik[m, o],   E_ik = sum_j cE_kj * pass_ijk   (tile i of row (c, kh, kw))
 //
-// on v_mfma_f32_16x16x32_bf16 (rows: 16 input pixels of one row; columns: the 16 channels; K: the 48 (k, o)
-// of one kernel position, two 32-deep steps), G split hi / mid / lo (fp32-accurate: What is a small
-// integer).  Per 128-input-pixel m-tile (4 input rows) and crossbar tile i the block builds G_i of the
-// six output rows those input rows read into an LDS "G patch" -- three bf16 planes [row][col][k][o] --
-// once; a wave then reads its A operand for kernel position (kh, kw) at the patch position shifted by
-// (kh, kw): one ds_read_b128 per plane and K-step, the shift an address offset.  The weight operand of
-// tile i (zero for the rows of other tiles) is staged per tile.  Every grad_x value is produced by one
-// lane, stored once after the LSQ backward: no fold pass, no ring, no atomics.
+// on v_mfma_f32_16x16x32_bf16 (rows: 16 input pixels of one row; columns: 16 channels; K: the 48 (k, o)
+// of one kernel position and 16-channel output half, two 32-deep steps), G split hi / mid / lo
+// (fp32-accurate: What is a small integer).  Per m-tile of 4 input rows, crossbar tile i and output half
+// h the block builds G_i of the six output rows those input rows read into an LDS "G patch" -- three
+// bf16 planes [row][col][k][o of the half] -- once; a wave then reads its A operand for kernel position
+// (kh, kw) at the patch position shifted by (kh, kw): one ds_read_b128 per plane and K-step, the shift an
+// address offset.  The weight operand of (tile i, half h) is staged per step (zero for the rows of other
+// tiles).  Waves: (16-pixel group, 16-channel input block); a wave whose channel block tile i does not
+// touch skips its MFMAs.  Every grad_x value is produced by one lane, stored once after the LSQ
+// backward: no fold pass, no ring, no atomics.
 #pragma once
 #include "cimq_v7.hip"
 
@@ -21,20 +23,27 @@ namespace cimq {
 struct X5 {
   int nmt;     // H / 4 * B: m-tiles of four input rows
   int tpi;     // m-tiles per image
+  int CBN;     // 16-channel input blocks (1 or 2) = 16-channel output halves
+  int NPG;     // 16-pixel groups per m-tile: W / 4 (8 or 4); waves = NPG * CBN = 8
 };
 
-// weight operand of (tile i, position p, K-step s), lane l: channel c = l & 15, K values
-// kappa = 32 s + 8 (l >> 4) + e (e < 8) = (k, o) = (kappa / 16, kappa % 16), int8(slice_k) of weight
-// (o, f = 9 c + p) as bf16 (wcy_item's values), zero for kappa >= 48 or f outside tile i
-// wg5[((i * 9 + p) * 2 + s) * 64 + l]
+// weight operand of (tile i, output half h, position p, K-step s, input block cb), lane l: channel
+// c = 16 cb + (l & 15), K values kappa = 32 s + 8 (l >> 4) + e (e < 8) = (k, o) = (kappa / 16, 16 h + kappa % 16),
+// int8(slice_k) of weight (o, f = 9 c + p) as bf16 (wcy_item's values), zero for kappa >= 48 or f outside
+// tile i: wg5[((((i * CBN + h) * 9 + p) * 2 + s) * CBN + cb) * 64 + l]
 template <typename WS>
 __device__ inline void wg5_item(const Geo& g, const WS& ws, v4i* __restrict__ wg5, int t) {
+  const int CBN = g.C / 16;
   const int lane = t & 63;
   int r = t >> 6;
+  const int cb = r % CBN;
+  r /= CBN;
   const int s = r & 1;
   r >>= 1;
-  const int p = r % 9, i = r / 9;
-  const int c = lane & 15;
+  const int p = r % 9;
+  r /= 9;
+  const int h = r % CBN, i = r / CBN;
+  const int c = 16 * cb + (lane & 15);
   const int f = c * 9 + p;
   const int flo = i * g.xbar, fhi = min(flo + g.xbar, g.K);
   const bool ok = c < g.C && f >= flo && f < fhi;
@@ -42,7 +51,7 @@ __device__ inline void wg5_item(const Geo& g, const WS& ws, v4i* __restrict__ wg
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int kap = 32 * s + 8 * (lane >> 4) + e;
-    const int k = kap >> 4, o = kap & 15;
+    const int k = kap >> 4, o = 16 * h + (kap & 15);
     float val = 0.f;
     if (ok && k < g.nbw) val = (float)to_i8_wrap(wslice(g, ws, f, k * g.Opad + o));
     wd[e >> 1] |= (uint32_t)bf16_bits(val) << (16 * (e & 1));
@@ -65,7 +74,8 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int WP = g.W + 2;
   const int PLANE = 6 * WP * 96;                        // bytes per plane
   const int OW5 = 3 * PLANE + 32;                       // weight operand offset
-  float* cel = reinterpret_cast<float*>(smem + OW5 + 18 * 1024);  // cE_kj
+  const int NW5 = 9 * 2 * v.CBN * 64;                   // weight fragments per (tile, half)
+  float* cel = reinterpret_cast<float*>(smem + OW5 + NW5 * 16);  // cE_kj
   float* red = cel + 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
@@ -85,20 +95,25 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const float scale = sw / 3.f;
   const float inv_sa = 1.f / sa;
   float gpart = 0.f;
-  // this wave's 16 input pixels: row 4 mt + (wave >> 1), columns 16 (wave & 1) .. +15
-  const int rl = wave >> 1, iw0 = 16 * (wave & 1);
+  // this wave: input block cb, 16 input pixels: row 4 mt + rl, columns iw0 .. iw0 + 15
+  const int cb = wave / v.NPG, pg = wave - cb * v.NPG;
+  const int gpr = g.W >> 4;  // pixel groups per row
+  const int rl = pg / gpr, iw0 = 16 * (pg - rl * gpr);
+  const int c_lo = 16 * cb, c_hi = 16 * cb + 15;
 
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
     const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
     v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < g.T; ++i) {
-      __syncthreads();  // the previous tile's (or m-tile's) MFMAs are done with the patch and weights
-      // the tile's weight operand
-      batched_copy<2>(9 * 2 * 64, reinterpret_cast<v4i*>(smem + OW5),
-                      [&](int idx) -> v4i { return wg5[(size_t)i * 9 * 2 * 64 + idx]; });
-      // G patch of output rows r0 - 1 .. r0 + 4: item = (row, col, 4 channels), channels fastest
+    for (int ih2 = 0; ih2 < g.T * v.CBN; ++ih2) {
+      const int i = ih2 / v.CBN, h = ih2 - i * v.CBN;  // tile, output half
+      __syncthreads();  // the previous step's (or m-tile's) MFMAs are done with the patch and weights
+      // the step's weight operand
+      batched_copy<2>(NW5, reinterpret_cast<v4i*>(smem + OW5),
+                      [&](int idx) -> v4i { return wg5[(size_t)ih2 * NW5 + idx]; });
+      // G patch of output rows r0 - 1 .. r0 + 4, output channels 16 h .. 16 h + 15: item = (row, col,
+      // 4 channels), channels fastest
       for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
-        const int oq = it & 3, rc = it >> 2, col = rc % g.W, row = rc / g.W;
+        const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc % g.W, row = rc / g.W;
         const int oh = r0 - 1 + row;
         float gv[4] = {0.f, 0.f, 0.f, 0.f};
         uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
@@ -110,7 +125,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           for (int e = 0; e < 4; ++e) gv[e] = gout[((size_t)b * g.O + 4 * oq + e) * g.P + pimg];
         }
         const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
-        uint8_t* px = smem + (size_t)(row * WP + col + 1) * 96 + 8 * oq;
+        uint8_t* px = smem + (size_t)(row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           float Gv[4];
@@ -153,8 +168,10 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
         }
       }
       __syncthreads();
-      // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes
-      const v4i* wb = reinterpret_cast<const v4i*>(smem + OW5) + lane;
+      // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes, unless tile i holds
+      // none of the block's rows (f = 9 c + p for c in c_lo .. c_hi)
+      if (9 * c_hi + 8 < i * g.xbar || 9 * c_lo >= (i + 1) * g.xbar) continue;
+      const v4i* wb = reinterpret_cast<const v4i*>(smem + OW5) + cb * 64 + lane;
 #pragma unroll
       for (int p = 0; p < 9; ++p) {
         const int kh = p / 3, kw = p - 3 * kh;
@@ -165,16 +182,16 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const v8bf ah = as_v8bf(*reinterpret_cast<const v4i*>(pa + 64 * s));
           const v8bf am = as_v8bf(*reinterpret_cast<const v4i*>(pa + PLANE + 64 * s));
           const v8bf al = as_v8bf(*reinterpret_cast<const v4i*>(pa + 2 * PLANE + 64 * s));
-          const v8bf w = as_v8bf(wb[(p * 2 + s) * 64]);
+          const v8bf w = as_v8bf(wb[(p * 2 + s) * v.CBN * 64]);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w, acc, 0, 0, 0);
         }
       }
     }
-    // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel r16: scale, LSQ activation backward, store
+    // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel c_lo + r16: scale, LSQ activation backward, store
     const int ih = r0 + rl, iw = iw0 + 4 * g4;
-    const size_t gi = (((size_t)b * g.C + r16) * g.H + ih) * g.W + iw;
+    const size_t gi = (((size_t)b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
     const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
     const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
     float o4[4];

@@ -805,7 +805,7 @@ inline PlanG5 g5_plan(const Geo& g) {
   return p;
 }
 
-// ---- grad_x of the w3a3 stride-1 16 -> 16-channel 32-wide layers, per input pixel (cimq_gx5.hip) ----
+// ---- grad_x of the w3a3 stride-1 16 -> 16 (32 x 32) / 32 -> 32 (16 x 16) layers, per input pixel (cimq_gx5.hip) ----
 struct PlanX5 {
   bool ok;
   X5 v;
@@ -820,15 +820,23 @@ inline PlanX5 x5_plan(const Geo& g) {
   if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsw != 1) return p;
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ || !g.onchw) return p;
   if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
-  if (g.C != 16 || g.O != 16 || g.W != 32 || g.H % 4 != 0 || g.Wo != g.W || g.Ho != g.H || g.T != 2) return p;
+  // 16 -> 16 at 32 x 32 (8 pixel groups x 1 channel block) or 32 -> 32 at 16 x 16 (4 x 2)
+  const bool c16 = g.C == 16 && g.O == 16 && g.W == 32, c32 = g.C == 32 && g.O == 32 && g.W == 16;
+  if (!(c16 || c32) || g.H % 4 != 0 || g.Wo != g.W || g.Ho != g.H || g.T != (9 * g.C + 127) / 128) return p;
   p.v.tpi = g.H / 4;
   p.v.nmt = g.B * p.v.tpi;
+  p.v.CBN = g.C / 16;
+  p.v.NPG = g.W / 4;
+  if (p.v.NPG * p.v.CBN != 8) return p;
   p.nblk = std::min(p.v.nmt, tune("GX5_GRID", 512));
-  p.lds = (size_t)3 * 6 * (g.W + 2) * 96 + 32 + 18 * 1024 + 32 * 4;
+  p.lds = (size_t)3 * 6 * (g.W + 2) * 96 + 32 + (size_t)9 * 2 * p.v.CBN * 1024 + 32 * 4;
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }
-inline size_t x5_frag_bytes(const Geo& g) { return x5_plan(g).ok ? (size_t)g.T * 9 * 2 * 64 * 16 : 0; }
+inline size_t x5_frag_bytes(const Geo& g) {
+  const PlanX5 p = x5_plan(g);
+  return p.ok ? (size_t)g.T * p.v.CBN * 9 * 2 * p.v.CBN * 64 * 16 : 0;
+}
 
 struct WsLayout {
   size_t gw_slab, ga_slab, gb_slab, ss_slab, qtab, lsq_part, gaq, gapart, wpart, bpo, gxu, total;
