@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 CIMQ_EINVAL = 1  # include/cimq.h error codes
 CIMQ_EUNSUPPORTED = 2
@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "cimq_pending_jobs",
     "cimq_module_prepare",
     "cimq_module_shift_supported",
+    "cimq_module_route",
     "cimq_module_shift_forward",
     "cimq_module_shift_backward",
     "cimq_alpha_init",
@@ -178,6 +179,8 @@ def _bind(lib):
     lib.cimq_module_prepare.argtypes = [ctypes.c_int, ctypes.POINTER(PrepareItem), _VP]
     lib.cimq_module_shift_supported.restype = ctypes.c_int
     lib.cimq_module_shift_supported.argtypes = [ctypes.POINTER(ConvDesc)]
+    lib.cimq_module_route.restype = ctypes.c_int
+    lib.cimq_module_route.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(ctypes.c_int)]
     lib.cimq_module_shift_forward.restype = ctypes.c_int
     lib.cimq_module_shift_forward.argtypes = [ctypes.POINTER(ConvDesc), ctypes.POINTER(LsqDesc)] + [_VP] * 12
     lib.cimq_module_shift_backward.restype = ctypes.c_int

@@ -629,6 +629,35 @@ int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const f
                              out, ctx, ws, stream);
 }
 
+int cimq_module_route(const cimq_conv_desc* d, int* route) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!route) return fail(CIMQ_EINVAL, "null route");
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  g.onchw = 1;  // the module path's layout (as module_forward_impl sets it)
+  route[0] = route[1] = route[2] = CIMQ_ROUTE_GENERAL;
+  // forward (module_forward_impl -> launch_fwd_any -> launch_fwd)
+  if (v3_plan(g).ok) {
+    route[0] = (fwd_actq_ok(g) && f5_plan(g).ok) ? CIMQ_ROUTE_FWD5 : CIMQ_ROUTE_V3;
+  } else if (dense_plan(g)) {
+    route[0] = CIMQ_ROUTE_DENSE;
+  }
+  // backward (dispatch_bwd_any)
+  if (v7_bwd(g)) {
+    if (c1_plan(g).ok) {
+      route[1] = route[2] = CIMQ_ROUTE_C1;
+    } else if (v9_plan(g).ok) {
+      route[1] = route[2] = CIMQ_ROUTE_FUSED;
+    } else if (v7_plan(g).ok) {
+      route[1] = x5_plan(g).ok ? CIMQ_ROUTE_GX5 : CIMQ_ROUTE_V7;
+      route[2] = g5_plan(g).ok ? CIMQ_ROUTE_GW5 : CIMQ_ROUTE_V7;
+    }
+  } else if (dense_plan(g)) {
+    route[1] = route[2] = CIMQ_ROUTE_DENSE;
+  }
+  return CIMQ_OK;
+}
+
 int cimq_module_shift_supported(const cimq_conv_desc* d) {
   Geo g;
   if (make_geo(d, &g) != CIMQ_OK) return 0;

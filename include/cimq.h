@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 11
+#define CIMQ_ABI_VERSION 12
 
 /* status codes */
 #define CIMQ_OK 0
@@ -200,6 +200,23 @@ int cimq_module_backward_params(const cimq_conv_desc* d, const cimq_lsq_desc* q,
  * (q->wprep NULL), no CIMQ_LSQ_SKIP_TAIL.  beta_cim / grad_beta_cim: [1, T, nbw, nba, 1, O] like
  * alpha_cim; CIMQ_LSQ_ACCUMULATE_GRADS adds into grad_beta_cim as well.  Since ABI 8. */
 int cimq_module_shift_supported(const cimq_conv_desc* d); /* 1 if the two calls below take d, else 0 */
+
+/* Which kernels cimq_module_forward / cimq_module_backward run for d (the library ADC, the module entry
+ * points): route[0] forward, route[1] grad_x, route[2] grad_w (+ grad_alpha_cim partials), each one of
+ * the CIMQ_ROUTE_* codes below.  Pure host query, no device work.  Returns 0, or an error status for a
+ * descriptor the module entry points refuse.  Since ABI 12. */
+enum {
+  CIMQ_ROUTE_GENERAL = 0,  /* the general kernels */
+  CIMQ_ROUTE_V3 = 1,       /* forward: cim_fwd_v3_kernel */
+  CIMQ_ROUTE_FWD5 = 2,     /* forward: cim_fwd5_kernel (slice-planar patch, round 5) */
+  CIMQ_ROUTE_V7 = 3,       /* grad_x: cim_bwd_gx_v8_kernel / grad_w: cim_bwd_gw_v7_kernel */
+  CIMQ_ROUTE_FUSED = 4,    /* grad_x and grad_w in cim_bwd_fused_kernel */
+  CIMQ_ROUTE_C1 = 5,       /* the w8a8 first conv: cim_bwd_c1_kernel (both) */
+  CIMQ_ROUTE_GX5 = 6,      /* grad_x: cim_bwd_gx5_kernel (per input pixel, round 5) */
+  CIMQ_ROUTE_GW5 = 7,      /* grad_w: cim_bwd_gw5_kernel (A-ready patch, round 5) */
+  CIMQ_ROUTE_DENSE = 8     /* the dense 1x1 path */
+};
+int cimq_module_route(const cimq_conv_desc* d, int* route);
 int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
                               const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
                               const float* beta_cim, const int8_t* binary_mask, const float* signed_act, float* out,

@@ -170,3 +170,34 @@ def test_pending_host_logic(lib):
     assert b"not initialised" in lib.cimq_last_error()
     assert lib.cimq_pending_jobs(p) == 0
     assert lib.cimq_pending_flush(None, None) == L.CIMQ_EINVAL
+
+
+def test_module_route_resnet20(lib):
+    """cimq_module_route (ABI 12): which kernels the module entry points run for each ResNet-20 layer of the
+    benchmark (bench.RESNET20, xbar 128, adc 1.5, B = 256) -- the round-5 kernels where their plans apply
+    (DESIGN.md section 4), the round-4 ones elsewhere.  A host query: no device work."""
+    import ctypes
+
+    import bench
+    want = {
+        "conv1": ("v3", "c1", "c1"),
+        "layer1.0.conv1": ("fwd5", "gx5", "gw5"),
+        "layer2.0.conv1": ("fwd5", "v7", "v7"),   # stride 2: the v8 / v7 pair
+        "layer2.0.conv2": ("fwd5", "gx5", "gw5"),
+        "layer3.0.conv1": ("v3", "v7", "v7"),     # stride 2, 64-pixel images at 32 channels: off fwd5's LDS budget
+        "layer3.0.conv2": ("fwd5", "fused", "fused"),
+    }
+    code = {0: "general", 1: "v3", 2: "fwd5", 3: "v7", 4: "fused", 5: "c1", 6: "gx5", 7: "gw5", 8: "dense"}  # CIMQ_ROUTE_*
+    got = {}
+    for name, c, o, h, s, nb in bench.RESNET20:
+        d = _desc(C=c, O=o, H=h, W=h, stride=(s, s), bits_w=nb, bits_a=nb, input_kind=L.CIMQ_INPUT_RAW_LSQ,
+                  lsq_qp=float(2 ** nb - 1))
+        r = (ctypes.c_int * 3)()
+        assert lib.cimq_module_route(ctypes.byref(d), r) == 0, lib.cimq_last_error()
+        got[name] = tuple(code[v] for v in r)
+    for name, w in want.items():
+        assert got[name] == w, (name, got[name])
+    # every 16 / 32-channel stride-1 layer of the benchmark takes all three round-5 kernels
+    for name, c, o, h, s, nb in bench.RESNET20:
+        if nb == 3 and s == 1 and c in (16, 32):
+            assert got[name] == ("fwd5", "gx5", "gw5"), (name, got[name])
