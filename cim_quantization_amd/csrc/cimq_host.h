@@ -714,6 +714,7 @@ inline Plan5 f5_plan(const Geo& g) {
   if (g.KH != 3 || g.KW != 3 || g.PH != 1 || g.PW != 1 || g.SH != g.SW || (g.SH != 1 && g.SH != 2)) return p;
   if (g.C % 16 != 0 || g.O % 16 != 0 || g.W % 4 != 0 || g.P % 16 != 0) return p;
   if (g.P >= 128 ? g.P % 128 != 0 : 128 % g.P != 0) return p;
+  if (g.M % 128 != 0) return p;  // whole 128-pixel m-tiles (B * P: whole images per m-tile when P < 128)
   if (g.Wo % 16 != 0 && 16 % g.Wo != 0) return p;
   F5& v = p.v;
   v.lwo = 0;
@@ -785,6 +786,7 @@ inline PlanG5 g5_plan(const Geo& g) {
   if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
   if (g.C % 16 != 0 || g.O % 16 != 0 || g.Wo % 4 != 0) return p;
   if (g.P >= 128 ? g.P % 128 != 0 : (128 % g.P != 0 || g.P % 16 != 0)) return p;
+  if (g.M % 128 != 0) return p;  // whole 128-pixel m-tiles
   if (g.T != (9 * g.C + 127) / 128 || !g.onchw) return p;
   G5& v = p.v;
   v.lwo = 0;
