@@ -634,6 +634,17 @@ int cimq_module_route(const cimq_conv_desc* d, int* route) {
   CIMQ_TRY(make_geo(d, &g));
   if (!route) return fail(CIMQ_EINVAL, "null route");
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
+  // the ctx / workspace layouts must not depend on state the entry points set only at launch (the
+  // module path's NCHW flag): cimq_query_sizes, the prologue and the kernels compute them separately
+  {
+    Geo g1 = g;
+    g1.onchw = 1;
+    const CtxLayout a = ctx_layout(g), c = ctx_layout(g1);
+    const WsLayout w0 = ws_layout(g), w1 = ws_layout(g1);
+    if (a.total != c.total || a.wbytes != c.wbytes || a.st != c.st || a.wg5 != c.wg5 || w0.total != w1.total ||
+        w0.nchunks_bwd != w1.nchunks_bwd || act_parts(g) != act_parts(g1))
+      return fail(CIMQ_EINVAL, "internal: layouts depend on the output layout flag");
+  }
   g.onchw = 1;  // the module path's layout (as module_forward_impl sets it)
   route[0] = route[1] = route[2] = CIMQ_ROUTE_GENERAL;
   // forward (module_forward_impl -> launch_fwd_any -> launch_fwd)

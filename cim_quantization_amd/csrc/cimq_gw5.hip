@@ -95,7 +95,13 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     const int pw = 16 * wave + 4 * g4;  // within the m-tile
     const int sl = pw / PI, pin0 = pw - sl * PI;  // image slot, pixel within the slot
     const int b = b0 + sl;
-    const float4 gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pin0);
+    float4 gq;
+    if (g.onchw) {
+      gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pin0);
+    } else {  // the Function path's [B, P, O]
+      const float* gp = gout + ((size_t)b * g.P + p0 + pin0) * g.O + o;
+      gq = make_float4(gp[0], gp[g.O], gp[2 * g.O], gp[3 * g.O]);
+    }
     uint32_t sq[2][4];
     {
       const size_t m = (size_t)b * g.P + p0 + pin0;

@@ -122,7 +122,8 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const size_t m = (size_t)b * g.P + pimg;
           s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + 4 * oq);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) gv[e] = gout[((size_t)b * g.O + 4 * oq + e) * g.P + pimg];
+          for (int e = 0; e < 4; ++e)
+            gv[e] = g.onchw ? gout[((size_t)b * g.O + 4 * oq + e) * g.P + pimg] : gout[m * g.O + 4 * oq + e];
         }
         const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
         uint8_t* px = smem + (size_t)(row * WP + col + 1) * 96 + 8 * (oq - 4 * h);

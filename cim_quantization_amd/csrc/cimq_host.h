@@ -787,7 +787,9 @@ inline PlanG5 g5_plan(const Geo& g) {
   if (g.C % 16 != 0 || g.O % 16 != 0 || g.Wo % 4 != 0) return p;
   if (g.P >= 128 ? g.P % 128 != 0 : (128 % g.P != 0 || g.P % 16 != 0)) return p;
   if (g.M % 128 != 0) return p;  // whole 128-pixel m-tiles
-  if (g.T != (9 * g.C + 127) / 128 || !g.onchw) return p;
+  // (no dependence on g.onchw: the ctx / workspace layouts are computed from the same Geo at query, prologue
+  // and launch time, and the module backward sets onchw only at launch; the kernel reads both layouts)
+  if (g.T != (9 * g.C + 127) / 128) return p;
   G5& v = p.v;
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
@@ -820,7 +822,7 @@ inline PlanX5 x5_plan(const Geo& g) {
   memset(&p, 0, sizeof(p));
   if (tune("GX5", 1) == 0) return p;
   if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsw != 1) return p;
-  if (g.input_kind != CIMQ_INPUT_RAW_LSQ || !g.onchw) return p;
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return p;  // (not g.onchw: see g5_plan)
   if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
   // 16 -> 16 at 32 x 32 (8 pixel groups x 1 channel block) or 32 -> 32 at 16 x 16 (4 x 2)
   const bool c16 = g.C == 16 && g.O == 16 && g.W == 32, c32 = g.C == 32 && g.O == 32 && g.W == 16;
