@@ -46,6 +46,8 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
                          reinterpret_cast<v4i*>(wreg(g, ctx) + L.wcy));
       CIMQ_TRY(check_hip("prep_wcy"));
     }
+    // cim_bwd_gx5_kernel's operand (x5_plan: the RAW_LSQ Function path runs that kernel too)
+    CIMQ_TRY(launch_prep_wg5(g, w_q, sw, ctx, s));
   }
   Params pp = params_of(g, ctx);
   if (need_params) {

@@ -62,6 +62,13 @@ __device__ inline void wg5_item(const Geo& g, const WS& ws, v4i* __restrict__ wg
 }
 
 #ifdef CIMQ_TU_GX5
+// the Function entry points' prologue (prep_all: w_q already quantised) builds the same operand
+__global__ void prep_wg5_kernel(Geo g, const float* __restrict__ w_q, const float* __restrict__ sw_p, int total,
+                                v4i* __restrict__ wg5) {
+  const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) wg5_item(g, ws, wg5, t);
+}
+
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 8)))
 void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i* __restrict__ wg5, Params pp,
                         const float* __restrict__ sw_p, const float* __restrict__ sa_p,

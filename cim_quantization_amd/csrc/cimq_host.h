@@ -1004,6 +1004,8 @@ int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, con
 // cimq_part_gx5.hip: grad_x (+ the fused act-LSQ backward) of the 16 -> 16-channel 32-wide layers (x5_plan)
 int launch_gx5(const Geo& g, const PlanX5& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
                const float* x, float* gx, uint8_t* ws, hipStream_t s);
+// ... and its weight operand from a quantised w_q (the Function entry points' prologue, prep_all)
+int launch_prep_wg5(const Geo& g, const float* w_q, const float* sw, uint8_t* ctx, hipStream_t s);
 // cimq_part_gw5.hip: grad_w + grad_alpha slabs of the w3a3 stride-1 16 / 32-channel layers (g5_plan)
 int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* gout, uint8_t* ws, hipStream_t s);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs

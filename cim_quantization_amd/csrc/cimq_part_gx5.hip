@@ -20,4 +20,13 @@ int launch_gx5(const Geo& g, const PlanX5& p, const uint8_t* ctx, const float* s
   return check_hip("cim_bwd_gx5");
 }
 
+int launch_prep_wg5(const Geo& g, const float* w_q, const float* sw, uint8_t* ctx, hipStream_t s) {
+  const int total = (int)(x5_frag_bytes(g) / 16);
+  if (total == 0) return CIMQ_OK;
+  CtxLayout L = ctx_layout(g);
+  hipLaunchKernelGGL(prep_wg5_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, g, w_q, sw, total,
+                     reinterpret_cast<v4i*>(wreg(g, ctx) + L.wg5));
+  return check_hip("prep_wg5");
+}
+
 }  // namespace cimq

@@ -88,6 +88,20 @@ def alpha_cim_terms(alpha, aa, nbits_alpha=8):
     return t
 
 
+def alpha_cim_report(ga, gr, alpha, aa, nbits_alpha=8):
+    """the worst entry of rel_err(ga, gr, alpha_cim_terms(alpha, aa)): index, max / min flag, values and terms
+    (the assertion message of the grad_alpha_cim checks)"""
+    t = alpha_cim_terms(alpha, aa, nbits_alpha)
+    ga, gr, a = (np.asarray(v, np.float64).reshape(-1) for v in (ga, gr, alpha))
+    t = t.reshape(-1)
+    aa = np.broadcast_to(np.asarray(aa, np.float64), np.shape(alpha)).reshape(-1)
+    r = np.abs(ga - gr) / (np.maximum(np.abs(gr), t) + 1e-30)
+    i = int(np.nanargmax(r))
+    kind = "max" if a[i] == a.max() else "min" if a[i] == a.min() else "inner"
+    return (f"worst entry {i} ({kind}, {int((a == a[i]).sum())} tied): mine {ga[i]:.9g} ref {gr[i]:.9g} "
+            f"terms {t[i]:.6g} aa {aa[i]:.6g} rel {r[i]:.3g}; entries over 1e-5: {int((r > 1e-5).sum())}/{r.size}")
+
+
 def normwise_err(mine, ref):
     """max |mine - ref| / max |ref| (gradients of contractions, which cancel elementwise)."""
     mine = np.asarray(mine, np.float64)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import alpha_cim_terms, rel_err
+from conftest import alpha_cim_report, alpha_cim_terms, rel_err
 from oracle import cim_module_oracle as cmo
 from oracle import cim_oracle as co
 from test_gpu_fullsize import _capture_oracle_ctx, _lsq_scalar_terms
@@ -66,7 +66,8 @@ def test_bench_graph_composition_vs_oracle(cuda_device, monkeypatch):
         assert rel_err(mine["weight"], gw_ref, aw.reshape(gw_ref.shape)) < 1e-5, (name, "grad_w")
         ga, gr = mine["alpha_cim"], om.alpha_cim.grad.numpy()
         # every entry; the max / min ones with the exact terms of the alpha quantiser's scale gradient
-        assert rel_err(ga, gr, alpha_cim_terms(om.alpha_cim.detach().numpy(), aa)) < 1e-5, (name, "grad_alpha_cim")
+        assert rel_err(ga, gr, alpha_cim_terms(om.alpha_cim.detach().numpy(), aa)) < 1e-5, \
+            (name, "grad_alpha_cim", alpha_cim_report(ga, gr, om.alpha_cim.detach().numpy(), aa))
         d = om.dbg
         qn_a, qp_a = co.lsq_act_params(bits)  # unsigned even for the signed first layer (lsq.py:537-538)
         qn_w, qp_w = co.lsq_weight_params(bits)

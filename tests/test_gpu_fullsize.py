@@ -24,7 +24,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import alpha_cim_terms, rel_err
+from conftest import alpha_cim_report, alpha_cim_terms, rel_err
 from oracle import cim_module_oracle as cmo
 from oracle import cim_oracle as co
 
@@ -81,7 +81,8 @@ def _check_elementwise(c, bm, g_nchw, out, oout, xt, ox, m, om):
     assert rel_err(np_(m.weight.grad), np_(om.weight.grad), aw.reshape(np_(om.weight.grad).shape)) < 1e-5, "grad_w"
     ga, gr = np_(m.alpha_cim.grad), np_(om.alpha_cim.grad)
     # every entry; the max / min ones with the exact terms of the alpha quantiser's scale gradient
-    assert rel_err(ga, gr, alpha_cim_terms(np_(om.alpha_cim), aa)) < 1e-5, "grad_alpha_cim"
+    assert rel_err(ga, gr, alpha_cim_terms(np_(om.alpha_cim), aa)) < 1e-5, \
+        "grad_alpha_cim: " + alpha_cim_report(ga, gr, np_(om.alpha_cim), aa)
 
 
 def _lsq_scalar_terms(x, g_xq, s, qn, qp, gscale):

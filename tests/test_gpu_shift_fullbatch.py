@@ -28,7 +28,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import alpha_cim_terms, rel_err
+from conftest import alpha_cim_report, alpha_cim_terms, rel_err
 from oracle import cim_module_oracle as cmo
 from oracle import cim_oracle as co
 
@@ -141,7 +141,8 @@ def _check(dev, monkeypatch, C, O, H, s, bits, B, seed, signed, repeat=True, shi
     ga, gr = np_(r1["ga"]), np_(om.alpha_cim.grad)
     # every entry, the max / min ones included: those also collect the alpha quantiser's scale gradient
     # (lsq.py:566-571), a sum over every entry whose exact |terms| alpha_cim_terms adds
-    assert rel_err(ga, gr, alpha_cim_terms(np_(om.alpha_cim), aa)) < 1e-5, "grad_alpha_cim"
+    assert rel_err(ga, gr, alpha_cim_terms(np_(om.alpha_cim), aa)) < 1e-5, \
+        "grad_alpha_cim: " + alpha_cim_report(ga, gr, np_(om.alpha_cim), aa)
     d = om.dbg
     t_act = _scalar_terms(x, np_(d["x_q"].grad), d["sa"].item(), 0, qp_a, 1.0 / math.sqrt(x.size * qp_a))
     t_w = _scalar_terms(w, np_(d["w_q"].grad), d["sw"].item(), qn_w, qp_w, 1.0 / math.sqrt(w.size * qp_w))
