@@ -32,6 +32,7 @@ constexpr int kF5MaxGrp = 4;  // tile groups
 // host-computed plan (cimq_host.h: f5_plan)
 struct F5 {
   int lwo;                 // log2(Wo)
+  int lwi;                 // log2(W)
   int IPM;                 // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
   int R, RH, WP;           // output rows per image slot, patch rows (R-1)*SH + 3, patch row length W + 2
   int NCBP;                // channel blocks one patch holds (the widest group's span)
@@ -39,11 +40,13 @@ struct F5 {
   int ntc;                 // (tile, channel-block) pairs
   int ngrp;                // tile groups
   int tcmax;               // most pairs in one group
-  unsigned char tc0[kF5MaxTc + 1];  // first pair of tile i (tc0[T] = ntc)
-  unsigned char tcb[kF5MaxTc];      // channel block of pair t
-  unsigned char gt0[kF5MaxGrp + 1]; // first tile of group q (gt0[ngrp] = T)
-  unsigned char gcb0[kF5MaxGrp], gcb1[kF5MaxGrp];  // channel-block span of group q
-  unsigned char gown[kF5MaxGrp];    // first channel block whose ctx words group q writes
+  // (int tables: the kernel indexes them with wave-uniform runtime indices, which scalar loads serve
+  // only at dword granularity -- byte tables became per-lane global loads of the kernel arguments)
+  int tc0[kF5MaxTc + 1];  // first pair of tile i (tc0[T] = ntc)
+  int tcb[kF5MaxTc];      // channel block of pair t
+  int gt0[kF5MaxGrp + 1]; // first tile of group q (gt0[ngrp] = T)
+  int gcb0[kF5MaxGrp], gcb1[kF5MaxGrp];  // channel-block span of group q
+  int gown[kF5MaxGrp];    // first channel block whose ctx words group q writes
 };
 
 // the part of the plan the weight prologue needs (kept small: it travels in every PrepJob)
@@ -94,6 +97,20 @@ __device__ inline void wf5_item(const Geo& g, const F5W& v, const WS& ws, v4i* _
   o.x = (int)wd[0]; o.y = (int)wd[1]; o.z = (int)wd[2]; o.w = (int)wd[3];
   wf5[t] = o;
 }
+
+// act_words_tab's table entry with the clamp moved after the rounding (rint(clamp(q, 0, Qp)) = clamp(rint(q),
+// 0, Qp) for integer bounds): v_cvt_i32_f32 saturates +-inf and the NaN test picks the table's NaN entry
+__device__ inline uint2 act_words_q5(float v, float sa, int qp, int nan_e, const uint32_t* lut) {
+  const float q = v / sa;
+  int e;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(e) : "v"(rintf(q)));
+  e = min(max(e, 0), qp);
+  e = (q == q) ? e : nan_e;
+  return *reinterpret_cast<const uint2*>(lut + 2 * e);
+}
+
+// n / d for 0 <= n < 2^20, d < 2^10 (inv = 1 / d in fp32): exact, no correction step needed
+__device__ inline int sdiv(int n, float inv) { return (int)(((float)n + 0.5f) * inv); }
 
 // LDS byte offset of the patch element (row, channel-block slot, col) of one image slot, slice 0
 // (slice j at + 16 j)
@@ -164,7 +181,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   }
   const int nan_e = (int)g.lsq_qp + 1;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;  // m-tiles per image
-  const size_t HW = (size_t)g.H * g.W;
+  const int HWi = g.H * g.W;
 
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
     const int b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
@@ -186,53 +203,52 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         // row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32
         // loads); quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices
         // into the slice planes, store the ctx words of owned rows and channel blocks
+        // (index arithmetic in 32 bits -- f5_plan bounds Nin -- with the divisions by the runtime QC and RH
+        // as exact float-reciprocal quotients, and every item's decomposition computed once)
         const int n = v.IPM * v.RH * QC * g.W;
+        const float invQC = 1.f / (float)QC, invRH = 1.f / (float)v.RH;
+        const int xbase = (b0 * g.C + 16 * cb0) * HWi + ih0 * g.W;  // element (image b0, channel 16 cb0, row ih0, col 0)
         for (int base = threadIdx.x; base < n; base += 2 * (int)blockDim.x) {
           float xv[2][4];
-          int meta[2];
+          int dsto[2], xo[2], ihs[2], qqs[2];
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int idx = base + u * (int)blockDim.x;
-            meta[u] = -1;
+            dsto[u] = -1;
 #pragma unroll
             for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
             if (idx < n) {
-              const int col = idx % g.W, r1 = idx / g.W;
-              const int qq = r1 % QC, r2 = r1 / QC;
-              const int row = r2 % v.RH, sl = r2 / v.RH;
-              const int ih = ih0 + row;
-              meta[u] = idx;
-              if ((unsigned)ih < (unsigned)g.H) {
-                const float* src = x + ((size_t)(b0 + sl) * g.C + 4 * (cb0 * 4 + qq)) * HW + (size_t)ih * g.W + col;
+              const int col = idx & (g.W - 1), r1 = idx >> v.lwi;
+              const int r2 = sdiv(r1, invQC), qq = r1 - r2 * QC;
+              const int sl = sdiv(r2, invRH), row = r2 - sl * v.RH;
+              ihs[u] = ih0 + row;
+              qqs[u] = qq;
+              dsto[u] = sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) + 4 * (qq & 3);
+              xo[u] = xbase + (sl * g.C + 4 * qq) * HWi + row * g.W + col;
+              if ((unsigned)ihs[u] < (unsigned)g.H) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) xv[u][e] = src[(size_t)e * HW];
+                for (int e = 0; e < 4; ++e) xv[u][e] = x[xo[u] + e * HWi];
               }
             }
           }
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
-            if (meta[u] < 0) continue;
-            const int idx = meta[u];
-            const int col = idx % g.W, r1 = idx / g.W;
-            const int qq = r1 % QC, r2 = r1 / QC;
-            const int row = r2 % v.RH, sl = r2 / v.RH;
-            const int ih = ih0 + row;
-            uint32_t* dst = reinterpret_cast<uint32_t*>(patch + sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) +
-                                                        4 * (qq & 3));
+            if (dsto[u] < 0) continue;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(patch + dsto[u]);
+            const int ih = ihs[u];
             if ((unsigned)ih >= (unsigned)g.H) {
               dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
               continue;
             }
             uint2 w[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) w[e] = act_words_tab(xv[u][e], sa, g.lsq_qp, nan_e, alut);
+            for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut);
             uint32_t P[4];
             tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
             dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
-            if (ih >= own_lo && ih < own_hi && cb0 + (qq >> 2) >= v.gown[q]) {
-              uint32_t* cbw = xcb + ((size_t)(b0 + sl) * g.C + 4 * (cb0 * 4 + qq)) * HW + (size_t)ih * g.W + col;
+            if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) cbw[(size_t)e * HW] = w[e].y;
+              for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
             }
           }
         }
@@ -242,9 +258,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
       const int tbase = v.tc0[v.gt0[q]];  // first pair of the group (its fragments start bfr)
       for (int i = v.gt0[q]; i < v.gt0[q + 1]; ++i) {
         v4i ps[9];
-#pragma unroll
-        for (int z = 0; z < 9; ++z) ps[z] = v4i{0, 0, 0, 0};
-        for (int tc = v.tc0[i]; tc < v.tc0[i + 1]; ++tc) {
+        // the tile's (pair, K-step) MFMAs; the first K-step of its first pair starts from the inline zero
+        // accumulator (no per-tile register clearing)
+        auto ksteps = [&](int tc, bool first) {
           const int cbo = (v.tcb[tc] - cb0) * v.WP * 48;
           const v4i* bt = reinterpret_cast<const v4i*>(smem) + (tc - tbase) * 9 * 64 + lane;  // LDS
 #pragma unroll
@@ -259,9 +275,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
             for (int k = 0; k < 3; ++k)
 #pragma unroll
               for (int j = 0; j < 3; ++j)
-                ps[k * 3 + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], ps[k * 3 + j], 0, 0, 0);
+                ps[k * 3 + j] = (first && s == 0)
+                                    ? __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], v4i{0, 0, 0, 0}, 0, 0, 0)
+                                    : __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], ps[k * 3 + j], 0, 0, 0);
           }
-        }
+        };
+        ksteps(v.tc0[i], true);  // f5_plan: every tile has at least one pair
+        for (int tc = v.tc0[i] + 1; tc < v.tc0[i + 1]; ++tc) ksteps(tc, false);
         // ADC + state bits of tile i: pairs kj = k*3 + j in descending order (bit 3*kj + {0,1,2} after
         // the last shift), the output summed in cim_fwd_v3_kernel's order
         uint32_t stw[4] = {0u, 0u, 0u, 0u};
@@ -306,16 +326,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         }
         const int o = ob * 16 + r16;
         if (o < g.O) {
-          uint32_t* s32 = st + ((size_t)i * g.M + m0) * g.O + o;
+          const int s0 = (i * g.M + m0) * g.O + o;  // 32-bit: f5_plan bounds T * M * O
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s32[(size_t)r * g.O] = stw[r];
+          for (int r = 0; r < 4; ++r) st[s0 + r * g.O] = stw[r];
         }
       }
     }
     const int o = ob * 16 + r16;
     if (o < g.O) {
       const int bb = m0 / g.P, pq = m0 - bb * g.P;
-      *reinterpret_cast<float4*>(out + ((size_t)bb * g.O + o) * g.P + pq) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(out + ((bb * g.O + o) * g.P + pq)) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     }
   }
 }

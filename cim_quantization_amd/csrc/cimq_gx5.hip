@@ -25,6 +25,7 @@ struct X5 {
   int tpi;     // m-tiles per image
   int CBN;     // 16-channel input blocks (1 or 2) = 16-channel output halves
   int NPG;     // 16-pixel groups per m-tile: W / 4 (8 or 4); waves = NPG * CBN = 8
+  int lw;      // log2(W)
 };
 
 // weight operand of (tile i, output half h, position p, K-step s, input block cb), lane l: channel
@@ -107,6 +108,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int gpr = g.W >> 4;  // pixel groups per row
   const int rl = pg / gpr, iw0 = 16 * (pg - rl * gpr);
   const int c_lo = 16 * cb, c_hi = 16 * cb + 15;
+  const int gstride = g.onchw ? g.P : 1;  // grad_out element stride between output channels
 
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
     const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
@@ -119,62 +121,52 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
                       [&](int idx) -> v4i { return wg5[(size_t)ih2 * NW5 + idx]; });
       // G patch of output rows r0 - 1 .. r0 + 4, output channels 16 h .. 16 h + 15: item = (row, col,
       // 4 channels), channels fastest
-      for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
-        const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc % g.W, row = rc / g.W;
-        const int oh = r0 - 1 + row;
-        float gv[4] = {0.f, 0.f, 0.f, 0.f};
-        uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
-        if ((unsigned)oh < (unsigned)g.Ho) {
-          const int pimg = oh * g.Wo + col;
-          const size_t m = (size_t)b * g.P + pimg;
-          s4 = *reinterpret_cast<const uint4*>(st + ((size_t)i * g.M + m) * g.O + 4 * oq);
+      // (32-bit offsets -- x5_plan bounds T * M * O -- W a power of two, the grad_out layout's element stride
+      // chosen once)
+      auto build = [&](auto stdc) {
+        constexpr bool STD = decltype(stdc)::value;
+        for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
+          const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
+          const int oh = r0 - 1 + row;
+          float gv[4] = {0.f, 0.f, 0.f, 0.f};
+          uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
+          if ((unsigned)oh < (unsigned)g.Ho) {
+            const int pimg = oh * g.Wo + col;
+            const int m = b * g.P + pimg;
+            s4 = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * oq));
+            const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : m * g.O + 4 * oq;
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            gv[e] = g.onchw ? gout[((size_t)b * g.O + 4 * oq + e) * g.P + pimg] : gout[m * g.O + 4 * oq + e];
-        }
-        const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
-        uint8_t* px = smem + (size_t)(row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          float Gv[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float E;
-            if (std_mask) {
-              E = (float)(__popc(sv[e] & pass_mask_k(k, 3)) << k);
-            } else {
-              E = 0.f;
-#pragma unroll
-              for (int j = 0; j < 3; ++j) E += ((sv[e] >> (3 * (k * 3 + j))) & 1u) ? cel[k * 3 + j] : 0.f;
-            }
-            Gv[e] = gv[e] * E;
+            for (int e = 0; e < 4; ++e) gv[e] = gout[go + e * gstride];
           }
-          // hi / mid / lo bf16 parts (split3x8's arithmetic on 4 values)
-          uint32_t ph[2], pm[2], plo[2];
+          const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+          uint8_t* px = smem + (row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            uint32_t hb[2], mb[2], lb[2];
+          for (int k = 0; k < 3; ++k) {
+            float Gv[4];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              const float vv = Gv[2 * h + u];
-              const __bf16 hh = (__bf16)vv;
-              const float r1 = vv - (float)hh;
-              const __bf16 mm = (__bf16)r1;
-              const float r2 = r1 - (float)mm;
-              const __bf16 ll = (__bf16)r2;
-              hb[u] = (uint32_t)__builtin_bit_cast(uint16_t, hh);
-              mb[u] = (uint32_t)__builtin_bit_cast(uint16_t, mm);
-              lb[u] = (uint32_t)__builtin_bit_cast(uint16_t, ll);
+            for (int e = 0; e < 4; ++e) {
+              float E;
+              if constexpr (STD) {
+                E = (float)(__popc(sv[e] & pass_mask_k(k, 3)) << k);
+              } else {
+                E = 0.f;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) E += ((sv[e] >> (3 * (k * 3 + j))) & 1u) ? cel[k * 3 + j] : 0.f;
+              }
+              Gv[e] = gv[e] * E;
             }
-            ph[h] = hb[0] | (hb[1] << 16);
-            pm[h] = mb[0] | (mb[1] << 16);
-            plo[h] = lb[0] | (lb[1] << 16);
+            // hi / mid / lo bf16 parts (split3x8's arithmetic), two values per conversion
+            uint32_t ph[2], pm[2], plo[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) split3_pk(Gv[2 * u], Gv[2 * u + 1], ph[u], pm[u], plo[u]);
+            *reinterpret_cast<uint2*>(px + 32 * k) = make_uint2(ph[0], ph[1]);
+            *reinterpret_cast<uint2*>(px + PLANE + 32 * k) = make_uint2(pm[0], pm[1]);
+            *reinterpret_cast<uint2*>(px + 2 * PLANE + 32 * k) = make_uint2(plo[0], plo[1]);
           }
-          *reinterpret_cast<uint2*>(px + 32 * k) = make_uint2(ph[0], ph[1]);
-          *reinterpret_cast<uint2*>(px + PLANE + 32 * k) = make_uint2(pm[0], pm[1]);
-          *reinterpret_cast<uint2*>(px + 2 * PLANE + 32 * k) = make_uint2(plo[0], plo[1]);
         }
-      }
+      };
+      if (std_mask) build(std::true_type{});
+      else build(std::false_type{});
       __syncthreads();
       // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes, unless tile i holds
       // none of the block's rows (f = 9 c + p for c in c_lo .. c_hi)
@@ -199,7 +191,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
     }
     // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel c_lo + r16: scale, LSQ activation backward, store
     const int ih = r0 + rl, iw = iw0 + 4 * g4;
-    const size_t gi = (((size_t)b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
+    const int gi = ((b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
     const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
     const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
     float o4[4];

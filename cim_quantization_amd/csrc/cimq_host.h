@@ -720,6 +720,12 @@ inline Plan5 f5_plan(const Geo& g) {
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
   if ((1 << v.lwo) != g.Wo) return p;
+  v.lwi = 0;
+  while ((1 << v.lwi) < g.W) ++v.lwi;
+  if ((1 << v.lwi) != g.W) return p;
+  // the kernel's element, state-word and output offsets are 32-bit
+  if ((long long)g.Nin >= (1LL << 31) || (long long)g.T * g.M * g.O >= (1LL << 31) || (long long)g.M * g.O >= (1LL << 31))
+    return p;
   const int PI = std::min(g.P, 128);
   v.IPM = 128 / PI;
   v.R = PI / g.Wo;
@@ -832,6 +838,10 @@ inline PlanX5 x5_plan(const Geo& g) {
   p.v.CBN = g.C / 16;
   p.v.NPG = g.W / 4;
   if (p.v.NPG * p.v.CBN != 8) return p;
+  p.v.lw = g.W == 32 ? 5 : 4;  // (c16: W 32, c32: W 16)
+  // 32-bit element / state-word offsets in the kernel
+  if ((long long)g.T * g.M * g.O >= (1LL << 31) || (long long)g.Nin >= (1LL << 31) || (long long)g.M * g.O >= (1LL << 31))
+    return p;
   p.nblk = std::min(p.v.nmt, tune("GX5_GRID", 512));
   p.lds = (size_t)3 * 6 * (g.W + 2) * 96 + 32 + (size_t)9 * 2 * p.v.CBN * 1024 + 32 * 4;
   p.ok = p.lds <= (size_t)80 * 1024;

@@ -259,17 +259,34 @@ __device__ inline void gather_xs(const uint8_t* patch, int rb, const int* ptab, 
 }
 
 // fp32 -> three bf16 parts (hi + mid + lo), 8 values -> 3 MFMA operands
+// (a, b) -> bf16 hi / mid / lo pairs, low half a: round-to-nearest-even conversions and exact fp32
+// remainders (hi + mid + lo reproduces a to fp32 accuracy), one v_cvt_pk_bf16_f32 per level for both values
+__device__ inline uint32_t pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ inline void split3_pk(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = pk_bf16(a, b);
+  float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
+  mid = pk_bf16(ra, rb);
+  ra = ra - __uint_as_float(mid << 16);
+  rb = rb - __uint_as_float(mid & 0xffff0000u);
+  lo = pk_bf16(ra, rb);
+}
 __device__ inline void split3x8(const float (&v)[8], v8bf& bh, v8bf& bm, v8bf& bl) {
+  v4i h, m, l;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 h = (__bf16)v[e];
-    const float r1 = v[e] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    const float r2 = r1 - (float)m;
-    bh[e] = h;
-    bm[e] = m;
-    bl[e] = (__bf16)r2;
+  for (int e = 0; e < 4; ++e) {
+    uint32_t a, b, c;
+    split3_pk(v[2 * e], v[2 * e + 1], a, b, c);
+    h[e] = (int)a;
+    m[e] = (int)b;
+    l[e] = (int)c;
   }
+  bh = __builtin_bit_cast(v8bf, h);
+  bm = __builtin_bit_cast(v8bf, m);
+  bl = __builtin_bit_cast(v8bf, l);
 }
 
 // literal (threshold-free) per-partial-sum paths, kept out of line: degenerate alpha / scales
