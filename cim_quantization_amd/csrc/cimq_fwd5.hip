@@ -172,120 +172,89 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   const int pl = wave * 16 + r16;
   const int slot = pl / PI, pin = pl - slot * PI;
   const int pix = slot * IMGB + f5_off(v.NCBP, v.WP, (pin >> v.lwo) * g.SH, 0, (pin & (Wo - 1)) * g.SW);
-  // (the three K-step offsets pix + f5_off(kh, 0, kw) of positions 4 s + g4 are recomputed per use: registers)
-  auto pat = [&](int s) {
+  int pat[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
     const int p = min(4 * s + g4, 8);
     const int kh = p / 3, kw = p - kh * 3;
-    return pix + f5_off(v.NCBP, v.WP, kh, 0, kw);
-  };
+    pat[s] = pix + f5_off(v.NCBP, v.WP, kh, 0, kw);
+  }
   const int nan_e = (int)g.lsq_qp + 1;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;  // m-tiles per image
   const int HWi = g.H * g.W;
 
-  // Units (m-tile, tile group q) in a software pipeline: the input rows of the next unit's first 2 x 512
-  // staging items are loaded into registers before the current unit's MFMAs; the rest of a large unit's
-  // items (stride-2 / 64-channel groups) are loaded at staging time.
-  // Row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32 loads);
-  // quantise (the prologue's own table), transpose 4 channels x 3 slices into the slice planes, store the
-  // ctx words of owned rows and channel blocks.  Index arithmetic in 32 bits (f5_plan bounds Nin), the
-  // divisions by the runtime QC and RH as exact float-reciprocal quotients.
-  struct Unit {
-    int b0, p0, ih0, own_lo, own_hi, cb0, QC, n, xbase;
-    float invQC;
-  };
-  auto unit_of = [&](int mt, int q) {
-    Unit u;
-    u.b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
-    u.p0 = g.P >= 128 ? (mt - u.b0 * tpi) * 128 : 0;
-    const int oh0 = u.p0 >> v.lwo;
-    u.ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
-    // input rows whose ctx words this m-tile writes: its output rows' stride spans, to the image end for
-    // its last m-tile (one output-channel block's blocks write them)
-    u.own_lo = ob == 0 ? oh0 * g.SH : 0;
-    u.own_hi = ob == 0 ? (u.p0 + PI >= g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
-    u.cb0 = v.gcb0[q];
-    u.QC = (v.gcb1[q] - u.cb0 + 1) * 4;  // staged 4-channel groups
-    u.n = v.IPM * v.RH * u.QC * g.W;
-    u.invQC = 1.f / (float)u.QC;
-    u.xbase = (u.b0 * g.C + 16 * u.cb0) * HWi + u.ih0 * g.W;  // element (image b0, channel 16 cb0, row ih0, col 0)
-    return u;
-  };
-  const float invRH = 1.f / (float)v.RH;
-  struct Item {
-    int dst, xo, ih, qq;
-  };
-  auto item_of = [&](const Unit& u, int idx) {
-    Item it;
-    const int col = idx & (g.W - 1), r1 = idx >> v.lwi;
-    const int r2 = sdiv(r1, u.invQC), qq = r1 - r2 * u.QC;
-    const int sl = sdiv(r2, invRH), row = r2 - sl * v.RH;
-    it.ih = u.ih0 + row;
-    it.qq = qq;
-    it.dst = sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) + 4 * (qq & 3);
-    it.xo = u.xbase + (sl * g.C + 4 * qq) * HWi + row * g.W + col;
-    return it;
-  };
-  auto load4 = [&](const Unit& u, int idx, float (&xv)[4]) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) xv[e] = 0.f;
-    if (idx < u.n) {
-      const Item it = item_of(u, idx);
-      if ((unsigned)it.ih < (unsigned)g.H) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = x[it.xo + e * HWi];
-      }
-    }
-  };
-  auto put = [&](const Unit& u, int q, int idx, const float (&xv)[4]) {
-    if (idx >= u.n) return;
-    const Item it = item_of(u, idx);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(patch + it.dst);
-    if ((unsigned)it.ih >= (unsigned)g.H) {
-      dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
-      return;
-    }
-    uint2 w[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[e], sa, nan_e - 1, nan_e, alut);
-    uint32_t P[4];
-    tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
-    dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
-    if (it.ih >= u.own_lo && it.ih < u.own_hi && u.cb0 + (it.qq >> 2) >= v.gown[q]) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xcb[it.xo + e * HWi] = w[e].y;
-    }
-  };
-  float xr[2][4];  // the prefetched items threadIdx.x and threadIdx.x + 512 of the next unit
-  auto fetch = [&](int mt, int q) {
-    const Unit u = unit_of(mt, q);
-    load4(u, threadIdx.x, xr[0]);
-    load4(u, threadIdx.x + (int)blockDim.x, xr[1]);
-  };
-
-  int mt = blockIdx.x, q = 0;
-  if (mt < v.nmt) fetch(mt, 0);
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  while (mt < v.nmt) {
-    const Unit u = unit_of(mt, q);
-    const int cb0 = u.cb0;
+  for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
+    const int b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
+    const int p0 = g.P >= 128 ? (mt - b0 * tpi) * 128 : 0;
+    const int oh0 = p0 >> v.lwo;
+    const int ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
+    // input rows whose ctx words this m-tile writes: its output rows' stride spans, to the image end
+    // for its last m-tile (one output-channel block's blocks write them)
+    const int own_lo = ob == 0 ? oh0 * g.SH : 0;
+    const int own_hi = ob == 0 ? (p0 + PI >= g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int m0 = mt * 128 + wave * 16 + 4 * g4;  // output pixel of acc[0] (flattened b*P + p)
-    __syncthreads();  // the previous unit's waves are done with the patch (and the fragments)
-    if (v.ngrp > 1) stage_b(q);
-    put(u, q, threadIdx.x, xr[0]);
-    put(u, q, threadIdx.x + (int)blockDim.x, xr[1]);
-    for (int idx = threadIdx.x + 2 * (int)blockDim.x; idx < u.n; idx += blockDim.x) {
-      float xv[4];
-      load4(u, idx, xv);
-      put(u, q, idx, xv);
-    }
-    __syncthreads();
-    int mt_n = mt, q_n = q + 1;
-    if (q_n == v.ngrp) {
-      q_n = 0;
-      mt_n = mt + (int)gridDim.x;
-    }
-    if (mt_n < v.nmt) fetch(mt_n, q_n);  // in flight during this unit's MFMAs
-    {
+    for (int q = 0; q < v.ngrp; ++q) {
+      const int cb0 = v.gcb0[q], ncb = v.gcb1[q] - cb0 + 1;
+      const int QC = ncb * 4;  // staged 4-channel groups
+      __syncthreads();  // the previous group's / m-tile's waves are done with the patch (and the fragments)
+      if (v.ngrp > 1) stage_b(q);
+      {
+        // row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32
+        // loads); quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices
+        // into the slice planes, store the ctx words of owned rows and channel blocks
+        // (index arithmetic in 32 bits -- f5_plan bounds Nin -- with the divisions by the runtime QC and RH
+        // as exact float-reciprocal quotients, and every item's decomposition computed once)
+        const int n = v.IPM * v.RH * QC * g.W;
+        const float invQC = 1.f / (float)QC, invRH = 1.f / (float)v.RH;
+        const int xbase = (b0 * g.C + 16 * cb0) * HWi + ih0 * g.W;  // element (image b0, channel 16 cb0, row ih0, col 0)
+        for (int base = threadIdx.x; base < n; base += 2 * (int)blockDim.x) {
+          float xv[2][4];
+          int dsto[2], xo[2], ihs[2], qqs[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int idx = base + u * (int)blockDim.x;
+            dsto[u] = -1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
+            if (idx < n) {
+              const int col = idx & (g.W - 1), r1 = idx >> v.lwi;
+              const int r2 = sdiv(r1, invQC), qq = r1 - r2 * QC;
+              const int sl = sdiv(r2, invRH), row = r2 - sl * v.RH;
+              ihs[u] = ih0 + row;
+              qqs[u] = qq;
+              dsto[u] = sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) + 4 * (qq & 3);
+              xo[u] = xbase + (sl * g.C + 4 * qq) * HWi + row * g.W + col;
+              if ((unsigned)ihs[u] < (unsigned)g.H) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xv[u][e] = x[xo[u] + e * HWi];
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            if (dsto[u] < 0) continue;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(patch + dsto[u]);
+            const int ih = ihs[u];
+            if ((unsigned)ih >= (unsigned)g.H) {
+              dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
+              continue;
+            }
+            uint2 w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut);
+            uint32_t P[4];
+            tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
+            dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
+            if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
+            }
+          }
+        }
+      }
+      __syncthreads();
+
       const int tbase = v.tc0[v.gt0[q]];  // first pair of the group (its fragments start bfr)
       for (int i = v.gt0[q]; i < v.gt0[q + 1]; ++i) {
         v4i ps[9];
@@ -296,7 +265,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
           const v4i* bt = reinterpret_cast<const v4i*>(smem) + (tc - tbase) * 9 * 64 + lane;  // LDS
 #pragma unroll
           for (int s = 0; s < 3; ++s) {
-            const uint8_t* pa = patch + pat(s) + cbo;
+            const uint8_t* pa = patch + pat[s] + cbo;
             v4i a[3], w[3];
 #pragma unroll
             for (int j = 0; j < 3; ++j) a[j] = *reinterpret_cast<const v4i*>(pa + 16 * j);
@@ -363,17 +332,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         }
       }
     }
-    if (q == v.ngrp - 1) {
-      const int o = ob * 16 + r16;
-      if (o < g.O) {
-        const int bb = m0 / g.P, pq = m0 - bb * g.P;
-        *reinterpret_cast<float4*>(out + ((bb * g.O + o) * g.P + pq)) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = 0.f;
+    const int o = ob * 16 + r16;
+    if (o < g.O) {
+      const int bb = m0 / g.P, pq = m0 - bb * g.P;
+      *reinterpret_cast<float4*>(out + ((bb * g.O + o) * g.P + pq)) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     }
-    mt = mt_n;
-    q = q_n;
   }
 }
 #endif  // CIMQ_TU_FWD5

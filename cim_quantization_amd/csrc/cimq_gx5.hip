@@ -110,108 +110,73 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int c_lo = 16 * cb, c_hi = 16 * cb + 15;
   const int gstride = g.onchw ? g.P : 1;  // grad_out element stride between output channels
 
-  // Software pipeline over the block's units (m-tile, step = (tile i, half h)): the global reads of the next
-  // unit -- its weight operand and the grad_out / state words of its G patch -- are issued into registers
-  // before the current unit's MFMAs, and written to LDS after the next barrier.
-  const int NSTEP = g.T * v.CBN;
-  const int NG = 6 * g.W * 4;  // G patch items (row, col, 4 channels) per unit: <= 2 per thread (x5_plan)
-  constexpr int WR = 5, GI = 2;
-  v4i wr[WR];
-  uint4 sr[GI];
-  float gr[GI][4];
-  auto fetch = [&](int mt, int ih2) {
-    const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;
-    const int i = ih2 / v.CBN, h = ih2 - i * v.CBN;
+  for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
+    const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
+    v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int ih2 = 0; ih2 < g.T * v.CBN; ++ih2) {
+      const int i = ih2 / v.CBN, h = ih2 - i * v.CBN;  // tile, output half
+      __syncthreads();  // the previous step's (or m-tile's) MFMAs are done with the patch and weights
+      // the step's weight operand
+      batched_copy<2>(NW5, reinterpret_cast<v4i*>(smem + OW5),
+                      [&](int idx) -> v4i { return wg5[(size_t)ih2 * NW5 + idx]; });
+      // G patch of output rows r0 - 1 .. r0 + 4, output channels 16 h .. 16 h + 15: item = (row, col,
+      // 4 channels), channels fastest
+      // (32-bit offsets -- x5_plan bounds T * M * O -- W a power of two, the grad_out layout's element stride
+      // chosen once)
+      auto build = [&](auto stdc) {
+        constexpr bool STD = decltype(stdc)::value;
+        for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
+          const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
+          const int oh = r0 - 1 + row;
+          float gv[4] = {0.f, 0.f, 0.f, 0.f};
+          uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
+          if ((unsigned)oh < (unsigned)g.Ho) {
+            const int pimg = oh * g.Wo + col;
+            const int m = b * g.P + pimg;
+            s4 = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * oq));
+            const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : m * g.O + 4 * oq;
 #pragma unroll
-    for (int r = 0; r < WR; ++r) {
-      const int idx = threadIdx.x + r * (int)blockDim.x;
-      if (idx < NW5) wr[r] = wg5[ih2 * NW5 + idx];
-    }
-#pragma unroll
-    for (int k = 0; k < GI; ++k) {
-      const int it = threadIdx.x + k * (int)blockDim.x;
-      sr[k] = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gr[k][e] = 0.f;
-      const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
-      const int oh = r0 - 1 + row;
-      if (it < NG && (unsigned)oh < (unsigned)g.Ho) {
-        const int pimg = oh * g.Wo + col;
-        const int m = b * g.P + pimg;
-        sr[k] = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * oq));
-        const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : m * g.O + 4 * oq;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) gr[k][e] = gout[go + e * gstride];
-      }
-    }
-  };
-  // the fetched unit into LDS: the weight operand, and the G patch of output rows r0 - 1 .. r0 + 4, output
-  // channels 16 h .. 16 h + 15 (three bf16 planes, hi / mid / lo)
-  auto commit = [&](int ih2, auto stdc) {
-    constexpr bool STD = decltype(stdc)::value;
-    const int h = ih2 - (ih2 / v.CBN) * v.CBN;
-#pragma unroll
-    for (int r = 0; r < WR; ++r) {
-      const int idx = threadIdx.x + r * (int)blockDim.x;
-      if (idx < NW5) reinterpret_cast<v4i*>(smem + OW5)[idx] = wr[r];
-    }
-#pragma unroll
-    for (int k = 0; k < GI; ++k) {
-      const int it = threadIdx.x + k * (int)blockDim.x;
-      if (it >= NG) continue;
-      const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
-      const uint32_t sv[4] = {sr[k].x, sr[k].y, sr[k].z, sr[k].w};
-      uint8_t* px = smem + (row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
-#pragma unroll
-      for (int kk = 0; kk < 3; ++kk) {
-        float Gv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float E;
-          if constexpr (STD) {
-            E = (float)(__popc(sv[e] & pass_mask_k(kk, 3)) << kk);
-          } else {
-            E = 0.f;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) E += ((sv[e] >> (3 * (kk * 3 + j))) & 1u) ? cel[kk * 3 + j] : 0.f;
+            for (int e = 0; e < 4; ++e) gv[e] = gout[go + e * gstride];
           }
-          Gv[e] = gr[k][e] * E;
-        }
-        // hi / mid / lo bf16 parts (split3x8's arithmetic), two values per conversion
-        uint32_t ph[2], pm[2], plo[2];
+          const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+          uint8_t* px = smem + (row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) split3_pk(Gv[2 * u], Gv[2 * u + 1], ph[u], pm[u], plo[u]);
-        *reinterpret_cast<uint2*>(px + 32 * kk) = make_uint2(ph[0], ph[1]);
-        *reinterpret_cast<uint2*>(px + PLANE + 32 * kk) = make_uint2(pm[0], pm[1]);
-        *reinterpret_cast<uint2*>(px + 2 * PLANE + 32 * kk) = make_uint2(plo[0], plo[1]);
-      }
-    }
-  };
-
-  int mt = blockIdx.x, ih2 = 0;
-  if (mt < v.nmt) fetch(mt, 0);
-  v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-  while (mt < v.nmt) {
-    const int i = ih2 / v.CBN;
-    __syncthreads();  // the previous unit's MFMAs are done with the patch and weights
-    if (std_mask) commit(ih2, std::true_type{});
-    else commit(ih2, std::false_type{});
-    __syncthreads();
-    int mt_n = mt, ih2_n = ih2 + 1;
-    if (ih2_n == NSTEP) {
-      ih2_n = 0;
-      mt_n = mt + (int)gridDim.x;
-    }
-    if (mt_n < v.nmt) fetch(mt_n, ih2_n);  // in flight during this unit's MFMAs
-    // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes, unless tile i holds
-    // none of the block's rows (f = 9 c + p for c in c_lo .. c_hi)
-    if (!(9 * c_hi + 8 < i * g.xbar || 9 * c_lo >= (i + 1) * g.xbar)) {
+          for (int k = 0; k < 3; ++k) {
+            float Gv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float E;
+              if constexpr (STD) {
+                E = (float)(__popc(sv[e] & pass_mask_k(k, 3)) << k);
+              } else {
+                E = 0.f;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) E += ((sv[e] >> (3 * (k * 3 + j))) & 1u) ? cel[k * 3 + j] : 0.f;
+              }
+              Gv[e] = gv[e] * E;
+            }
+            // hi / mid / lo bf16 parts (split3x8's arithmetic), two values per conversion
+            uint32_t ph[2], pm[2], plo[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) split3_pk(Gv[2 * u], Gv[2 * u + 1], ph[u], pm[u], plo[u]);
+            *reinterpret_cast<uint2*>(px + 32 * k) = make_uint2(ph[0], ph[1]);
+            *reinterpret_cast<uint2*>(px + PLANE + 32 * k) = make_uint2(pm[0], pm[1]);
+            *reinterpret_cast<uint2*>(px + 2 * PLANE + 32 * k) = make_uint2(plo[0], plo[1]);
+          }
+        }
+      };
+      if (std_mask) build(std::true_type{});
+      else build(std::false_type{});
+      __syncthreads();
+      // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes, unless tile i holds
+      // none of the block's rows (f = 9 c + p for c in c_lo .. c_hi)
+      if (9 * c_hi + 8 < i * g.xbar || 9 * c_lo >= (i + 1) * g.xbar) continue;
       const v4i* wb = reinterpret_cast<const v4i*>(smem + OW5) + cb * 64 + lane;
 #pragma unroll
       for (int p = 0; p < 9; ++p) {
         const int kh = p / 3, kw = p - 3 * kh;
         // output pixel (oh, ow) = (ih + 1 - kh, iw + 1 - kw): patch row rl + 2 - kh, column iw + 2 - kw
-        const uint8_t* pa = smem + ((rl + 2 - kh) * WP + iw0 + r16 + 2 - kw) * 96 + 16 * g4;
+        const uint8_t* pa = smem + (size_t)((rl + 2 - kh) * WP + iw0 + r16 + 2 - kw) * 96 + 16 * g4;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const v8bf ah = as_v8bf(*reinterpret_cast<const v4i*>(pa + 64 * s));
@@ -224,33 +189,27 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
         }
       }
     }
-    if (ih2 == NSTEP - 1) {
-      // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel c_lo + r16: scale, LSQ activation backward, store
-      const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;
-      const int ih = r0 + rl, iw = iw0 + 4 * g4;
-      const int gi = ((b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
-      const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
-      const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
-      float o4[4];
+    // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel c_lo + r16: scale, LSQ activation backward, store
+    const int ih = r0 + rl, iw = iw0 + 4 * g4;
+    const int gi = ((b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
+    const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
+    const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+    float o4[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gqv = acc[r] * scale;
-        // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v8_kernel
-        const float y1 = xv[r] / sa;
-        const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
-        const float rr2 = rintf(clv);
-        const float rp = (rr2 - clv) + clv;
-        const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
-        const float gy = pass ? gqv * sa : 0.f;
-        o4[r] = pass ? gqv : 0.f;
-        gpart += gqv * rp;
-        gpart += -(gy * (y1 * inv_sa));
-      }
-      *reinterpret_cast<float4*>(gx + gi) = make_float4(o4[0], o4[1], o4[2], o4[3]);
-      acc = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) {
+      const float gqv = acc[r] * scale;
+      // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v8_kernel
+      const float y1 = xv[r] / sa;
+      const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
+      const float rr2 = rintf(clv);
+      const float rp = (rr2 - clv) + clv;
+      const bool pass = (y1 >= 0.f) && (y1 <= g.lsq_qp);
+      const float gy = pass ? gqv * sa : 0.f;
+      o4[r] = pass ? gqv : 0.f;
+      gpart += gqv * rp;
+      gpart += -(gy * (y1 * inv_sa));
     }
-    mt = mt_n;
-    ih2 = ih2_n;
+    *reinterpret_cast<float4*>(gx + gi) = make_float4(o4[0], o4[1], o4[2], o4[3]);
   }
   // the block's d sa partial (fixed order: lanes, then waves)
   for (int o = 32; o > 0; o >>= 1) gpart += __shfl_xor(gpart, o);

@@ -839,8 +839,6 @@ inline PlanX5 x5_plan(const Geo& g) {
   p.v.NPG = g.W / 4;
   if (p.v.NPG * p.v.CBN != 8) return p;
   p.v.lw = g.W == 32 ? 5 : 4;  // (c16: W 32, c32: W 16)
-  // the kernel's registers of the next unit: <= 2 G patch items and <= 5 weight fragments per thread
-  if (6 * g.W * 4 > 2 * 512 || 9 * 2 * p.v.CBN * 64 > 5 * 512) return p;
   // 32-bit element / state-word offsets in the kernel
   if ((long long)g.T * g.M * g.O >= (1LL << 31) || (long long)g.Nin >= (1LL << 31) || (long long)g.M * g.O >= (1LL << 31))
     return p;
