@@ -23,8 +23,12 @@
 
 namespace cimq {
 
+// n / d for 0 <= n < 2^20, d < 2^10 (inv = 1 / d in fp32): exact
+__device__ inline int sdiv5(int n, float inv) { return (int)(((float)n + 0.5f) * inv); }
+
 struct G5 {
   int lwo;     // log2(Wo)
+  int lwi;     // log2(W)
   int IPM;     // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
   int R, RH, WP;  // output rows per image slot, staged input rows R + 2, patch row length W + 2
   int nmt;     // M / 128
@@ -84,6 +88,8 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 
   const int Wo = 1 << v.lwo;
   const int PI = g.P < 128 ? g.P : 128;  // pixels per image slot
+  const int HWi = g.H * g.W;
+  const float invRH = 1.f / (float)v.RH, invIPM = 1.f / (float)v.IPM;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;
   const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
   for (int mt = mt_lo; mt < mt_hi; ++mt) {
@@ -114,7 +120,10 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     {
       // A-ready patch: input rows oh0 - 1 .. oh0 + R of each image slot, the block's 16 channels; item =
       // (c, slot, row, col)
+      // (W a power of two; the divisions by RH and CH as exact float-reciprocal quotients; 32-bit offsets:
+      // g5_plan bounds Nin)
       const int n = 16 * CH * g.W;
+      const int xb = (b0 * g.C + 16 * cb) * HWi + (oh0 - 1) * g.W;  // (image b0, channel 16 cb, row oh0 - 1)
       for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
         uint32_t wv[4];
         int dst[4];
@@ -124,11 +133,12 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
           dst[u] = -1;
           wv[u] = 0u;
           if (idx < n) {
-            const int col = idx % g.W, cr = idx / g.W, row = cr % v.RH, c = cr / CH, slt = (cr / v.RH) - c * v.IPM;
+            const int col = idx & (g.W - 1), cr = idx >> v.lwi;
+            const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
+            const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
             const int ih = oh0 - 1 + row;
             dst[u] = cr * v.WP + col + 1;
-            if ((unsigned)ih < (unsigned)g.H)
-              wv[u] = xcb[(((size_t)(b0 + slt) * g.C + 16 * cb + c) * g.H + ih) * g.W + col];
+            if ((unsigned)ih < (unsigned)g.H) wv[u] = xcb[xb + (slt * g.C + c) * HWi + row * g.W + col];
           }
         }
 #pragma unroll

@@ -800,6 +800,8 @@ inline PlanG5 g5_plan(const Geo& g) {
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
   if ((1 << v.lwo) != g.Wo || 128 % g.Wo != 0) return p;
+  v.lwi = v.lwo;  // stride 1: W == Wo
+  if ((long long)g.Nin >= (1LL << 31)) return p;  // 32-bit element offsets in the staging
   v.IPM = 128 / std::min(g.P, 128);
   v.R = std::min(g.P, 128) / g.Wo;
   v.RH = v.R + 2;
