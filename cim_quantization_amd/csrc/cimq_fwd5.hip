@@ -33,6 +33,7 @@ constexpr int kF5MaxGrp = 4;  // tile groups
 struct F5 {
   int lwo;                 // log2(Wo)
   int lwi;                 // log2(W)
+  int codes;               // 1: the ctx holds one code byte per element (ctx_codes: grad_w is cim_bwd_gw5_kernel)
   int IPM;                 // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
   int R, RH, WP;           // output rows per image slot, patch rows (R-1)*SH + 3, patch row length W + 2
   int NCBP;                // channel blocks one patch holds (the widest group's span)
@@ -100,12 +101,13 @@ __device__ inline void wf5_item(const Geo& g, const F5W& v, const WS& ws, v4i* _
 
 // act_words_tab's table entry with the clamp moved after the rounding (rint(clamp(q, 0, Qp)) = clamp(rint(q),
 // 0, Qp) for integer bounds): v_cvt_i32_f32 saturates +-inf and the NaN test picks the table's NaN entry
-__device__ inline uint2 act_words_q5(float v, float sa, int qp, int nan_e, const uint32_t* lut) {
+__device__ inline uint2 act_words_q5(float v, float sa, int qp, int nan_e, const uint32_t* lut, int& code) {
   const float q = v / sa;
   int e;
   asm("v_cvt_i32_f32 %0, %1" : "=v"(e) : "v"(rintf(q)));
   e = min(max(e, 0), qp);
   e = (q == q) ? e : nan_e;
+  code = e;
   return *reinterpret_cast<const uint2*>(lut + 2 * e);
 }
 
@@ -120,7 +122,7 @@ __device__ inline int f5_off(int NCB, int WP, int row, int cb, int col) { return
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void cim_fwd5_kernel(
     Geo g, F5 v, const v4i* __restrict__ wf5, Params pp, const float* __restrict__ sw_p,
     const float* __restrict__ sa_p, const float* __restrict__ x, const float* __restrict__ sgn_p,
-    float* __restrict__ out, uint32_t* __restrict__ st, uint32_t* __restrict__ xcb) {
+    float* __restrict__ out, uint32_t* __restrict__ st, uint32_t* __restrict__ xcb, uint32_t* __restrict__ cal) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int ob = blockIdx.y;
   const int nfr = v.ntc * 9;  // this block's fragments ([pair][s][k], 64 lanes each)
@@ -165,6 +167,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     reinterpret_cast<uint32_t*>(patch + (rcb * v.WP + (side ? v.WP - 1 : 0)) * 48)[q] = 0u;
   }
   act_lut_build_q<3>(g, sa, sgn, alut);  // entries 0 .. Qp + 1 (NaN), then the block barrier
+  // ctx codes: the table grad_w expands them with (code e -> ctx word), written once per launch
+  if (v.codes && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x) cal[t] = alut[2 * t + 1];
 
   // this lane's A-operand pixel (image slot, output row / col) and its three position offsets
   const int Wo = 1 << v.lwo;
@@ -241,14 +246,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
               continue;
             }
             uint2 w[4];
+            int code[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut);
+            for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut, code[e]);
             uint32_t P[4];
             tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
             dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
             if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
+              if (v.codes) {  // one byte per element: grad_w expands it through the same word table
+                uint8_t* cb8 = reinterpret_cast<uint8_t*>(xcb);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
+                for (int e = 0; e < 4; ++e) cb8[xo[u] + e * HWi] = (uint8_t)code[e];
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
+              }
             }
           }
         }

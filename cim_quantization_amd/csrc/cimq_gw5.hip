@@ -29,6 +29,8 @@ __device__ inline int sdiv5(int n, float inv) { return (int)(((float)n + 0.5f) *
 struct G5 {
   int lwo;     // log2(Wo)
   int lwi;     // log2(W)
+  int codes;   // 1: the ctx holds one activation code byte per element (the forward was cim_fwd5_kernel with
+               // ctx_codes): expanded through the act word table, as the forward's staging does
   int IPM;     // images per 128-pixel m-tile (1: the m-tile is R output rows of one image)
   int R, RH, WP;  // output rows per image slot, staged input rows R + 2, patch row length W + 2
   int nmt;     // M / 128
@@ -39,13 +41,16 @@ struct G5 {
 #ifdef CIMQ_TU_GW5
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
-                        const float* __restrict__ gout, float* __restrict__ gw_slab, float* __restrict__ ga_slab) {
+                        const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
+                        float* __restrict__ ga_slab) {
   // block = (pixel chunk, input-channel block cb, output block ob): the 9 16-row blocks of rows
   // f = 144 cb .. 144 cb + 143 (the 16 channels of cb at every (kh, kw)), which touch at most two tiles
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint2* pat = reinterpret_cast<uint2*>(smem);  // [16 channels][IPM][RH][WP] of (xhat_0 | xhat_1 << 16, xhat_2)
   const int CH = v.IPM * v.RH;  // patch rows per channel
   float* cdl = reinterpret_cast<float*>(smem + (size_t)16 * CH * v.WP * 8);  // cD_kj
+  // code -> ctx word (v.codes), addressed as a byte offset from smem (LDS loads, not generic ones)
+  const int alut_off = 16 * CH * v.WP * 8 + 16 * 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const int cb = blockIdx.y / g.OB16, ob = blockIdx.y - cb * g.OB16;
@@ -53,6 +58,10 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int i_lo = (144 * cb) / 128, i_hi = (144 * cb + 143) / 128;  // tiles of the block's rows (xbar 128)
   const int ntl = i_hi - i_lo + 1;
   for (int t = threadIdx.x; t < 9; t += blockDim.x) cdl[t] = pp.ckj[18 + t];
+  // the forward's backward-word table (ctx, written by cim_fwd5_kernel): code e -> ctx word
+  if (v.codes)
+    for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x)
+      *reinterpret_cast<uint32_t*>(smem + alut_off + 4 * t) = cal[t];
   // padding columns 0 and WP-1: zero once
   for (int t = threadIdx.x; t < 16 * CH * 2; t += blockDim.x) {
     const int side = t & 1, cr = t >> 1;
@@ -127,23 +136,31 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
         uint32_t wv[4];
         int dst[4];
+        bool inb[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int idx = base + u * (int)blockDim.x;
           dst[u] = -1;
           wv[u] = 0u;
+          inb[u] = false;
           if (idx < n) {
             const int col = idx & (g.W - 1), cr = idx >> v.lwi;
             const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
             const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
             const int ih = oh0 - 1 + row;
             dst[u] = cr * v.WP + col + 1;
-            if ((unsigned)ih < (unsigned)g.H) wv[u] = xcb[xb + (slt * g.C + c) * HWi + row * g.W + col];
+            if ((unsigned)ih < (unsigned)g.H) {
+              inb[u] = true;
+              const int xi = xb + (slt * g.C + c) * HWi + row * g.W + col;
+              // (a code byte, expanded below through the LDS table, or the word itself)
+              wv[u] = v.codes ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[xi] : xcb[xi];
+            }
           }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (dst[u] < 0) continue;
+          if (v.codes && inb[u]) wv[u] = *reinterpret_cast<const uint32_t*>(smem + alut_off + 4 * (int)wv[u]);
           // int8 ctx slices (lsq.py:160 truncation, wrapped) -> exact bf16 (the high half of the fp32)
           const uint32_t f0 = __float_as_uint((float)(int8_t)(wv[u] & 0xFFu));
           const uint32_t f1 = __float_as_uint((float)(int8_t)((wv[u] >> 8) & 0xFFu));

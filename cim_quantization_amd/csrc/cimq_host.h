@@ -157,7 +157,7 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, wfrag, wf5, wg5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
+  size_t xcode, xhat, alut, wfrag, wf5, wg5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
@@ -189,6 +189,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.wbytes = o;
   L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);  // forward slice bytes
   L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
+  L.alut = o; o = align256(o + (size_t)4 * 260);         // ctx codes: code -> ctx word (ctx_codes)
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
   // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three
@@ -812,7 +813,8 @@ inline PlanG5 g5_plan(const Geo& g) {
   const int want = std::max(1, tune("GW5_BLOCKS", 512) / p.pairs);
   v.nst = std::max(1, (v.nmt + want - 1) / want);
   v.nchunks = (v.nmt + v.nst - 1) / v.nst;
-  p.lds = std::max((size_t)16 * v.IPM * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64;
+  // the A-ready patch (or the wave-sum buffer), then cD_kj (16 floats) and the code -> word table (260)
+  p.lds = std::max((size_t)16 * v.IPM * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64 + 4 * 260;
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }
@@ -852,6 +854,16 @@ inline PlanX5 x5_plan(const Geo& g) {
 inline size_t x5_frag_bytes(const Geo& g) {
   const PlanX5 p = x5_plan(g);
   return p.ok ? (size_t)g.T * p.v.CBN * 9 * 2 * p.v.CBN * 64 * 16 : 0;
+}
+
+// The module path's ctx as ONE activation-code byte per element (instead of the 4-byte backward word):
+// where the forward is cim_fwd5_kernel (which quantises the activation itself) and the layer's grad_w
+// is cim_bwd_gw5_kernel (dispatch_bwd_any's order: c1, fused, then the v7 pair), the only ctx reader.
+// Decided at launch: g.onchw is the module entry points' flag (the Function path's prologue writes words).
+// (c1_plan / v9_plan are declared above ws_layout.)
+inline bool ctx_codes(const Geo& g) {
+  return g.onchw && fwd_actq_ok(g) && f5_plan(g).ok && v7_bwd(g) && !c1_plan(g).ok && !v9_plan(g).ok &&
+         g5_plan(g).ok;
 }
 
 struct WsLayout {

@@ -164,6 +164,17 @@ __global__ __launch_bounds__(256) void prep_module_kernel(Geo g, LsqArgs q, Modu
   module_prep_weights(g, q, a, (int)blockIdx.x, nwblk, red);
 }
 
+// The job of block b in a packed launch: the number of job starts blk0[1 .. n-1] at or below b, counted
+// over the whole (fixed-size) table -- independent scalar loads of the kernel arguments and a compare
+// chain, instead of a search loop whose every step waits on the previous step's argument load
+template <int NJ>
+__device__ inline int job_of(const int (&blk0)[NJ + 1], int n, int b) {
+  int j = 0;
+#pragma unroll
+  for (int t = 1; t < NJ; ++t) j += (t < n && b >= blk0[t]) ? 1 : 0;
+  return j;
+}
+
 // The weight side of several layers' prologues in one launch (cimq_module_prepare): a layer's
 // weight work is a few latency-bound blocks, so packing the layers of a network into one grid
 // pays that latency once instead of once per layer.  The jobs travel as kernel arguments.
@@ -183,8 +194,7 @@ static_assert(sizeof(PrepPack) <= 4000, "PrepPack exceeds the kernel-argument bu
 
 __global__ __launch_bounds__(256) void prep_weights_many_kernel(PrepPack p) {
   __shared__ float4 red4[16];
-  int j = 0;
-  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  const int j = job_of<kPrepJobs>(p.blk0, p.n, (int)blockIdx.x);
   module_prep_weights(p.job[j].g, p.job[j].q, p.job[j].a, (int)blockIdx.x - p.blk0[j], p.job[j].nwblk,
                       reinterpret_cast<float*>(red4));
 }
@@ -245,8 +255,7 @@ __device__ inline Geo geo_of(const TailGeo& t) {
 
 __global__ __launch_bounds__(1024, 8) void module_tail_many_kernel(TailPack p) {
   __shared__ __attribute__((aligned(16))) float red[4 * 1024];
-  int j = 0;
-  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  const int j = job_of<kTailJobs>(p.blk0, p.n, (int)blockIdx.x);
   const TailJob& jb = p.job[j];
   const Geo g = geo_of(jb.t);
   const int b = (int)blockIdx.x - p.blk0[j];
@@ -269,8 +278,7 @@ static_assert(sizeof(FinishPack) <= 4000, "FinishPack exceeds the kernel-argumen
 // one block per job, cdiv(nalpha, 1024) for a wide alpha_cim (module_finish_wide_block)
 __global__ __launch_bounds__(1024) void module_finish_many_kernel(FinishPack p) {
   __shared__ __attribute__((aligned(16))) float red[16 * 8];
-  int j = 0;
-  while (j + 1 < p.n && (int)blockIdx.x >= p.blk0[j + 1]) ++j;
+  const int j = job_of<kFinishJobs>(p.blk0, p.n, (int)blockIdx.x);
   const FinishJob& jb = p.job[j];
   if (jb.a.gapart) module_finish_wide_block(jb.q, jb.a, red, (int)blockIdx.x - p.blk0[j]);
   else module_finish_block(jb.q, jb.a, red);

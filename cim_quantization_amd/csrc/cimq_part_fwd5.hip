@@ -16,9 +16,12 @@ int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, con
   const int per_ob = std::max(1, tune("FWD5_GRID", 512) / g.OB16);
   dim3 grid(std::min(p.v.nmt, per_ob), g.OB16);
   const int slot = prof_begin(KID_FWD_V7, g, s);
-  hipLaunchKernelGGL(kern, grid, dim3(512), p.lds, s, g, p.v, reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wf5),
+  F5 v = p.v;
+  v.codes = ctx_codes(g) ? 1 : 0;  // one code byte per ctx element (grad_w is cim_bwd_gw5_kernel)
+  hipLaunchKernelGGL(kern, grid, dim3(512), p.lds, s, g, v, reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wf5),
                      params_of(g, ctx), sw, sa, aq->x, aq->signed_act, out,
-                     reinterpret_cast<uint32_t*>(ctx + L.st), reinterpret_cast<uint32_t*>(ctx + L.xhat));
+                     reinterpret_cast<uint32_t*>(ctx + L.st), reinterpret_cast<uint32_t*>(ctx + L.xhat),
+                     reinterpret_cast<uint32_t*>(ctx + L.alut));
   prof_end(slot, s);
   return check_hip("cim_fwd5");
 }

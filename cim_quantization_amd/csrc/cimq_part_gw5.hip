@@ -13,10 +13,12 @@ int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* g
   auto kern = cim_bwd_gw5_kernel;
   CIMQ_TRY(set_lds(kern, p.lds));
   const int slot = prof_begin(KID_GW_V7, g, s);
-  hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(512), p.lds, s, g, p.v,
+  G5 v = p.v;
+  v.codes = ctx_codes(g) ? 1 : 0;  // the forward wrote code bytes (cim_fwd5_kernel on the module path)
+  hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(512), p.lds, s, g, v,
                      reinterpret_cast<const uint32_t*>(ctx + L.st), reinterpret_cast<const uint32_t*>(ctx + L.xhat),
-                     params_of(g, const_cast<uint8_t*>(ctx)), gout, reinterpret_cast<float*>(ws + W.gw_slab),
-                     reinterpret_cast<float*>(ws + W.ga_slab));
+                     params_of(g, const_cast<uint8_t*>(ctx)), gout, reinterpret_cast<const uint32_t*>(ctx + L.alut),
+                     reinterpret_cast<float*>(ws + W.gw_slab), reinterpret_cast<float*>(ws + W.ga_slab));
   prof_end(slot, s);
   return check_hip("cim_bwd_gw5");
 }
