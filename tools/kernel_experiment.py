@@ -45,6 +45,12 @@ VARIANTS = {
     # slab sums (tools/tail_sweep.sh with CIMQ_LIB_PATH=<variant lib>)
     "tail_noepi": ["CIMQ_EXP_TAIL_NOEPI"],
     "tail_noslab": ["CIMQ_EXP_TAIL_NOSLAB"],
+    # round 5: the per-input-pixel grad_x (cimq_gx5.hip) without the G build / with one A read per K-step
+    # (LDS read traffic / 9 and one plane) / without the MFMAs
+    "gx5_nobuild": ["CIMQ_EXP_GX5_NOBUILD"],
+    "gx5_noaread": ["CIMQ_EXP_GX5_NOAREAD"],
+    "gx5_nomfma": ["CIMQ_EXP_GX5_NOMFMA"],
+    "gx5_noaread_nomfma": ["CIMQ_EXP_GX5_NOAREAD", "CIMQ_EXP_GX5_NOMFMA"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
