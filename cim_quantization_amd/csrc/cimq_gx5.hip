@@ -110,11 +110,34 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int c_lo = 16 * cb, c_hi = 16 * cb + 15;
   const int gstride = g.onchw ? g.P : 1;  // grad_out element stride between output channels
 
+  const int NG = 6 * g.W * 4;  // G patch items (row, col, 4 channels): <= 2 per thread (x5_plan)
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
     const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
     v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-    for (int ih2 = 0; ih2 < g.T * v.CBN; ++ih2) {
-      const int i = ih2 / v.CBN, h = ih2 - i * v.CBN;  // tile, output half
+    // grad_out of the m-tile's G-patch items, both output halves: read once here, used by every tile's step
+    // (it was re-read per tile)
+    float gvr[2][2][4];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int it = threadIdx.x + k * (int)blockDim.x;
+        const int oq = (it & 3) + 4 * hh, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
+        const int oh = r0 - 1 + row;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gvr[hh][k][e] = 0.f;
+        if (hh < v.CBN && it < NG && (unsigned)oh < (unsigned)g.Ho) {
+          const int pimg = oh * g.Wo + col;
+          const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : (b * g.P + pimg) * g.O + 4 * oq;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) gvr[hh][k][e] = gout[go + e * gstride];
+        }
+      }
+    for (int i = 0; i < g.T; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h >= v.CBN) break;
+      const int ih2 = i * v.CBN + h;  // step: tile i, output half h
       __syncthreads();  // the previous step's (or m-tile's) MFMAs are done with the patch and weights
       // the step's weight operand
       batched_copy<2>(NW5, reinterpret_cast<v4i*>(smem + OW5),
@@ -125,18 +148,17 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
       // chosen once)
       auto build = [&](auto stdc) {
         constexpr bool STD = decltype(stdc)::value;
-        for (int it = threadIdx.x; it < 6 * g.W * 4; it += blockDim.x) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int it = threadIdx.x + kk * (int)blockDim.x;
+          if (it >= NG) continue;
           const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
           const int oh = r0 - 1 + row;
-          float gv[4] = {0.f, 0.f, 0.f, 0.f};
+          const float* gv = gvr[h][kk];
           uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
           if ((unsigned)oh < (unsigned)g.Ho) {
-            const int pimg = oh * g.Wo + col;
-            const int m = b * g.P + pimg;
+            const int m = b * g.P + oh * g.Wo + col;
             s4 = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * oq));
-            const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : m * g.O + 4 * oq;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) gv[e] = gout[go + e * gstride];
           }
           const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
           uint8_t* px = smem + (row * WP + col + 1) * 96 + 8 * (oq - 4 * h);

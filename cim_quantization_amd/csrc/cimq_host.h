@@ -843,6 +843,7 @@ inline PlanX5 x5_plan(const Geo& g) {
   p.v.NPG = g.W / 4;
   if (p.v.NPG * p.v.CBN != 8) return p;
   p.v.lw = g.W == 32 ? 5 : 4;  // (c16: W 32, c32: W 16)
+  if (6 * g.W * 4 > 2 * 512) return p;  // the kernel keeps <= 2 G-patch items' grad_out per thread
   // 32-bit element / state-word offsets in the kernel
   if ((long long)g.T * g.M * g.O >= (1LL << 31) || (long long)g.Nin >= (1LL << 31) || (long long)g.M * g.O >= (1LL << 31))
     return p;
