@@ -118,25 +118,30 @@ __device__ inline int sdiv(int n, float inv) { return (int)(((float)n + 0.5f) * 
 // (slice j at + 16 j)
 __device__ inline int f5_off(int NCB, int WP, int row, int cb, int col) { return ((row * NCB + cb) * WP + col) * 48; }
 
-#ifdef CIMQ_TU_FWD5  // non-template kernel: defined in its launcher's translation unit only
-__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4))) void cim_fwd5_kernel(
+#ifdef CIMQ_TU_FWD5  // defined in its launcher's translation unit only
+// NOB 16-channel output blocks per block (512 threads each): the NOB halves share the block's staged
+// activation patch (f5_plan: NOB = 2 where OB16 is even, one 1024-thread block per CU)
+template <int NOB>
+__global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amdgpu_waves_per_eu(4, 4))) void cim_fwd5_kernel(
     Geo g, F5 v, const v4i* __restrict__ wf5, Params pp, const float* __restrict__ sw_p,
     const float* __restrict__ sa_p, const float* __restrict__ x, const float* __restrict__ sgn_p,
     float* __restrict__ out, uint32_t* __restrict__ st, uint32_t* __restrict__ xcb, uint32_t* __restrict__ cal) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int ob = blockIdx.y;
-  const int nfr = v.ntc * 9;  // this block's fragments ([pair][s][k], 64 lanes each)
-  // smem: weight fragments [<= tcmax][s][k][64] (v4i), then the tables below
-  int4* prm = reinterpret_cast<int4*>(smem + (size_t)v.tcmax * 9 * 1024);    // [i][j][k][16] (all tiles)
-  float* cfl = reinterpret_cast<float*>(prm + g.T * 9 * 16);                 // same order
-  uint32_t* alut = reinterpret_cast<uint32_t*>(cfl + g.T * 9 * 16);          // [Qp + 2][fwd, bwd]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int obl = wave >> 3, pw = wave & 7;  // this wave's output block within the block, its pixel group
+  const int ob = blockIdx.y * NOB + obl;
+  const int nfr = v.ntc * 9;  // one output block's fragments ([pair][s][k], 64 lanes each)
+  const size_t WB = (size_t)v.tcmax * 9 * 1024;  // LDS bytes of one output block's staged fragments
+  // smem: weight fragments [NOB][<= tcmax][s][k][64] (v4i), then the tables below
+  int4* prm = reinterpret_cast<int4*>(smem + NOB * WB);                      // [obl][i][j][k][16] (all tiles)
+  float* cfl = reinterpret_cast<float*>(prm + NOB * g.T * 9 * 16);           // same order
+  uint32_t* alut = reinterpret_cast<uint32_t*>(cfl + NOB * g.T * 9 * 16);    // [Qp + 2][fwd, bwd]
   // [img][RH][NCBP][WP][3][16]: a 16-aligned byte offset from smem (an integer round trip through
   // uintptr_t would turn the LDS pointer into a generic one: flat loads that wait on vmcnt too)
-  const size_t poff0 = (size_t)v.tcmax * 9 * 1024 + (size_t)g.T * 9 * 16 * (16 + 4) + (size_t)2 * ((int)g.lsq_qp + 2) * 4;
+  const size_t poff0 = NOB * WB + (size_t)NOB * g.T * 9 * 16 * (16 + 4) + (size_t)2 * ((int)g.lsq_qp + 2) * 4;
   uint8_t* patch = smem + ((poff0 + 15) & ~(size_t)15);
   const int IMGB = v.RH * v.NCBP * v.WP * 48;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
   const float sw = *sw_p, sa = *sa_p;
   const bool literal = pp.flags[0] != 0;
@@ -145,18 +150,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   // the weight fragments of group q (pairs tc0[gt0[q]] .. tc0[gt0[q+1]])
   auto stage_b = [&](int q) {
     const int a = v.tc0[v.gt0[q]], n = (v.tc0[v.gt0[q + 1]] - a) * 9 * 64;
-    const v4i* src = wf5 + ((size_t)ob * nfr + a * 9) * 64;
-    batched_copy<4>(n, reinterpret_cast<v4i*>(smem), [&](int idx) -> v4i { return src[idx]; });
+#pragma unroll
+    for (int h = 0; h < NOB; ++h) {
+      const v4i* src = wf5 + ((size_t)(blockIdx.y * NOB + h) * nfr + a * 9) * 64;
+      batched_copy<4>(n, reinterpret_cast<v4i*>(smem + h * WB), [&](int idx) -> v4i { return src[idx]; });
+    }
   };
-  // thresholds and coefficients of every tile (small): resident
-  batched_copy<2>(g.T * 9 * 16, prm, [&](int idx) -> int4 {
-    const int o = ob * 16 + (idx & 15), q = idx >> 4;  // q = i*9 + j*3 + k
+  // thresholds and coefficients of every tile (small): resident ([obl][T * 9 * 16])
+  const int TQ = g.T * 9 * 16;
+  batched_copy<2>(NOB * TQ, prm, [&](int idx0) -> int4 {
+    const int h = idx0 / TQ, idx = idx0 - h * TQ;
+    const int o = (blockIdx.y * NOB + h) * 16 + (idx & 15), q = idx >> 4;  // q = i*9 + j*3 + k
     const int i = q / 9, jk = q - i * 9, j = jk / 3, k = jk - j * 3;
     const int pi = pidx(g, i, j, k, o);
     return literal ? make_int4(0, 0, 0, 0) : make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
   });
-  batched_copy<2>(g.T * 9 * 16, cfl, [&](int idx) -> float {
-    const int o = ob * 16 + (idx & 15), q = idx >> 4;
+  batched_copy<2>(NOB * TQ, cfl, [&](int idx0) -> float {
+    const int h = idx0 / TQ, idx = idx0 - h * TQ;
+    const int o = (blockIdx.y * NOB + h) * 16 + (idx & 15), q = idx >> 4;
     const int i = q / 9, jk = q - i * 9, j = jk / 3, k = jk - j * 3;
     return literal ? 0.f : pp.coef[pidx(g, i, j, k, o)];
   });
@@ -174,7 +185,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   // this lane's A-operand pixel (image slot, output row / col) and its three position offsets
   const int Wo = 1 << v.lwo;
   const int PI = g.P < 128 ? g.P : 128;  // pixels per image slot
-  const int pl = wave * 16 + r16;
+  const int pl = pw * 16 + r16;
   const int slot = pl / PI, pin = pl - slot * PI;
   const int pix = slot * IMGB + f5_off(v.NCBP, v.WP, (pin >> v.lwo) * g.SH, 0, (pin & (Wo - 1)) * g.SW);
   int pat[3];
@@ -195,10 +206,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     const int ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
     // input rows whose ctx words this m-tile writes: its output rows' stride spans, to the image end
     // for its last m-tile (one output-channel block's blocks write them)
-    const int own_lo = ob == 0 ? oh0 * g.SH : 0;
-    const int own_hi = ob == 0 ? (p0 + PI >= g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
+    // (the staging is block-wide: the block holding output block 0 writes them)
+    const int own_lo = blockIdx.y == 0 ? oh0 * g.SH : 0;
+    const int own_hi = blockIdx.y == 0 ? (p0 + PI >= g.P ? g.H : (oh0 + v.R) * g.SH) : 0;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int m0 = mt * 128 + wave * 16 + 4 * g4;  // output pixel of acc[0] (flattened b*P + p)
+    const int m0 = mt * 128 + pw * 16 + 4 * g4;  // output pixel of acc[0] (flattened b*P + p)
     for (int q = 0; q < v.ngrp; ++q) {
       const int cb0 = v.gcb0[q], ncb = v.gcb1[q] - cb0 + 1;
       const int QC = ncb * 4;  // staged 4-channel groups
@@ -274,7 +286,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         // accumulator (no per-tile register clearing)
         auto ksteps = [&](int tc, bool first) {
           const int cbo = (v.tcb[tc] - cb0) * v.WP * 48;
-          const v4i* bt = reinterpret_cast<const v4i*>(smem) + (tc - tbase) * 9 * 64 + lane;  // LDS
+          const v4i* bt = reinterpret_cast<const v4i*>(smem + obl * WB) + (tc - tbase) * 9 * 64 + lane;  // LDS
 #pragma unroll
           for (int s = 0; s < 3; ++s) {
             const uint8_t* pa = patch + pat[s] + cbo;
@@ -302,7 +314,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
           for (int k = 2; k >= 0; --k) {
 #pragma unroll
             for (int j = 2; j >= 0; --j) {
-              const int pc = (i * 9 + j * 3 + k) * 16 + r16;
+              const int pc = obl * TQ + (i * 9 + j * 3 + k) * 16 + r16;
               const int4 pv = prm[pc];
               const float cf = cfl[pc];
 #pragma unroll

@@ -701,6 +701,7 @@ struct Plan5 {
   bool ok;
   F5 v;
   size_t lds;
+  int nob;  // 16-channel output blocks per workgroup (the kernel's template argument)
 };
 
 inline Plan5 f5_plan(const Geo& g) {
@@ -744,11 +745,15 @@ inline Plan5 f5_plan(const Geo& g) {
     }
   }
   v.tc0[g.T] = (unsigned char)v.ntc;
+  // output blocks per workgroup: two (a 1024-thread block per CU, sharing the activation patch) where
+  // OB16 is even, else one (two 512-thread blocks per CU)
+  p.nob = (g.OB16 % 2 == 0 && tune("FWD5_NOB2", 1)) ? 2 : 1;
   // tile groups: greedy, while the block's LDS (the widest group's fragments and channel span) fits
-  // two blocks per CU
-  const size_t fixed = (size_t)g.T * 9 * 16 * (16 + 4) + a16((size_t)2 * ((int)g.lsq_qp + 2) * 4) + 16;
-  const size_t budget = (size_t)tune("FWD5_LDS_KB", 80) * 1024;
-  auto need = [&](int tcm, int ncb) { return fixed + (size_t)tcm * 9 * 1024 + (size_t)v.IPM * v.RH * ncb * v.WP * 48; };
+  const size_t fixed = (size_t)p.nob * g.T * 9 * 16 * (16 + 4) + a16((size_t)2 * ((int)g.lsq_qp + 2) * 4) + 16;
+  const size_t budget = (size_t)(p.nob == 2 ? tune("FWD5_LDS2_KB", 150) : tune("FWD5_LDS_KB", 80)) * 1024;
+  auto need = [&](int tcm, int ncb) {
+    return fixed + (size_t)p.nob * tcm * 9 * 1024 + (size_t)v.IPM * v.RH * ncb * v.WP * 48;
+  };
   v.ngrp = 0;
   v.tcmax = 0;
   v.NCBP = 0;

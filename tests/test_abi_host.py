@@ -184,7 +184,7 @@ def test_module_route_resnet20(lib):
         "layer1.0.conv1": ("fwd5", "gx5", "gw5"),
         "layer2.0.conv1": ("fwd5", "v7", "v7"),   # stride 2: the v8 / v7 pair
         "layer2.0.conv2": ("fwd5", "gx5", "gw5"),
-        "layer3.0.conv1": ("v3", "v7", "v7"),     # stride 2, 64-pixel images at 32 channels: off fwd5's LDS budget
+        "layer3.0.conv1": ("fwd5", "v7", "v7"),   # stride 2: fwd5 with two output blocks per workgroup (its larger LDS budget)
         "layer3.0.conv2": ("fwd5", "fused", "fused"),
     }
     code = {0: "general", 1: "v3", 2: "fwd5", 3: "v7", 4: "fused", 5: "c1", 6: "gx5", 7: "gw5", 8: "dense"}  # CIMQ_ROUTE_*
