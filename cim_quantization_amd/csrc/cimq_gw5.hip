@@ -127,12 +127,14 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     }
     __syncthreads();  // the previous m-tile's waves are done with the patch
     {
-      // A-ready patch: input rows oh0 - 1 .. oh0 + R of each image slot, the block's 16 channels; item =
+      // A-ready patch: input rows oh0 * SH - 1 .. (oh0 + R - 1) * SH + 1 of each image slot, the block's 16
+      // channels; item =
       // (c, slot, row, col)
       // (W a power of two; the divisions by RH and CH as exact float-reciprocal quotients; 32-bit offsets:
       // g5_plan bounds Nin)
       const int n = 16 * CH * g.W;
-      const int xb = (b0 * g.C + 16 * cb) * HWi + (oh0 - 1) * g.W;  // (image b0, channel 16 cb, row oh0 - 1)
+      const int ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
+      const int xb = (b0 * g.C + 16 * cb) * HWi + ih0 * g.W;  // (image b0, channel 16 cb, row ih0)
       for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
         uint32_t wv[4];
         int dst[4];
@@ -147,7 +149,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
             const int col = idx & (g.W - 1), cr = idx >> v.lwi;
             const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
             const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
-            const int ih = oh0 - 1 + row;
+            const int ih = ih0 + row;
             dst[u] = cr * v.WP + col + 1;
             if ((unsigned)ih < (unsigned)g.H) {
               inb[u] = true;
@@ -176,7 +178,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
       const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
       const int pin = pin0 + e0;  // within the image slot
-      const int poff = (sl * v.RH + (pin >> v.lwo)) * v.WP + (pin & (Wo - 1));
+      const int poff = (sl * v.RH + (pin >> v.lwo) * g.SH) * v.WP + (pin & (Wo - 1)) * g.SW;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (q >= ntl) break;
@@ -215,7 +217,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
         for (int fb = 0; fb < 9; ++fb) {
           if (atl[fb] != q) continue;  // uniform: the 16-row blocks of this tile
-          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + 1];
+          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + g.SW];
           const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);

@@ -795,7 +795,13 @@ inline PlanG5 g5_plan(const Geo& g) {
   memset(&p, 0, sizeof(p));
   if (tune("GW5", 1) == 0) return p;
   if (!v7_bwd(g) || g.variant != VAR_LIBRARY || g.NBP != 4 || g.nbw != 3 || g.nba != 3 || g.bsa != 1) return p;
-  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
+  if (g.KH != 3 || g.KW != 3 || g.SH != g.SW || (g.SH != 1 && g.SH != 2) || g.PH != 1 || g.PW != 1 ||
+      g.xbar != 128)
+    return p;
+  if (g.W != g.Wo * g.SH || g.H != g.Ho * g.SH) return p;  // (stride 2: even input sides)
+  // stride 2 measured slower than cim_bwd_gw_v7_kernel (51.5 vs 43 us per launch on ResNet-20's two
+  // transition layers: 17 staged rows for 8 output rows); kept for the tuning build
+  if (g.SH == 2 && tune("GW5_S2", 0) == 0) return p;
   if (g.C % 16 != 0 || g.O % 16 != 0 || g.Wo % 4 != 0) return p;
   if (g.P >= 128 ? g.P % 128 != 0 : (128 % g.P != 0 || g.P % 16 != 0)) return p;
   if (g.M % 128 != 0) return p;  // whole 128-pixel m-tiles
@@ -806,11 +812,11 @@ inline PlanG5 g5_plan(const Geo& g) {
   v.lwo = 0;
   while ((1 << v.lwo) < g.Wo) ++v.lwo;
   if ((1 << v.lwo) != g.Wo || 128 % g.Wo != 0) return p;
-  v.lwi = v.lwo;  // stride 1: W == Wo
+  v.lwi = v.lwo + (g.SH == 2 ? 1 : 0);  // W = Wo * SH
   if ((long long)g.Nin >= (1LL << 31)) return p;  // 32-bit element offsets in the staging
   v.IPM = 128 / std::min(g.P, 128);
   v.R = std::min(g.P, 128) / g.Wo;
-  v.RH = v.R + 2;
+  v.RH = (v.R - 1) * g.SH + 3;
   v.WP = g.W + 2;
   v.nmt = g.M / 128;
   p.pairs = (g.C / 16) * g.OB16;

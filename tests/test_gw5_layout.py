@@ -13,14 +13,16 @@ def pass_mask_j(j):
     return sum(1 << (3 * (k * 3 + j)) for k in range(3))
 
 
-@pytest.mark.parametrize("C,O,H", [(16, 16, 32), (32, 32, 16), (64, 64, 8)])
-def test_gw5_plan_grad_w_and_alpha(C, O, H):
-    rng = np.random.default_rng(C + O + H)
-    W = Wo = H
-    P = H * H
+@pytest.mark.parametrize("C,O,H,S", [(16, 16, 32, 1), (32, 32, 16, 1), (64, 64, 8, 1), (16, 32, 32, 2), (32, 64, 16, 2)])
+def test_gw5_plan_grad_w_and_alpha(C, O, H, S):
+    rng = np.random.default_rng(C + O + H + S)
+    W = H
+    Ho = Wo = H // S
+    P = Ho * Wo
     PI = min(P, 128)
     IPM, R = 128 // PI, PI // Wo
-    RH, WP, CH = R + 2, W + 2, IPM * (R + 2)
+    RH = (R - 1) * S + 3
+    WP, CH = W + 2, IPM * RH
     K = 9 * C
     T = -(-K // 128)
     B = IPM * max(1, P // 128) if P < 128 else 1  # one m-tile's images
@@ -44,7 +46,7 @@ def test_gw5_plan_grad_w_and_alpha(C, O, H):
             s = st[i, m]
             for j in range(3):
                 D = np.array([bin(int(v) & pass_mask_j(j)).count("1") << j for v in s])
-                ref_gw[f] += xp[b, c, oh + kh, ow + kw, j] * g[b, :, p] * D
+                ref_gw[f] += xp[b, c, oh * S + kh, ow * S + kw, j] * g[b, :, p] * D
         for i in range(T):
             s = st[i, m]
             for kj in range(9):
@@ -77,7 +79,7 @@ def test_gw5_plan_grad_w_and_alpha(C, O, H):
                         pw = 16 * wave + 4 * g4
                         sl, pin0 = pw // PI, pw % PI
                         pin = pin0 + 2 * s
-                        poff = (sl * RH + pin // Wo) * WP + pin % Wo
+                        poff = (sl * RH + (pin // Wo) * S) * WP + (pin % Wo) * S
                         o = ob * 16 + r16
                         for e, pp in enumerate((pin, pin + 1)):
                             m = sl * P + pp
@@ -96,7 +98,7 @@ def test_gw5_plan_grad_w_and_alpha(C, O, H):
                             kh, kw = divmod(q9, 3)
                             aoff = (c * CH + kh) * WP + kw
                             A[fb, lane, 0:4] = pat[aoff + poff]
-                            A[fb, lane, 4:8] = pat[aoff + poff + 1]
+                            A[fb, lane, 4:8] = pat[aoff + poff + S]
                     for fb in range(9):
                         q = (144 * cb + 16 * fb) // 128 - i_lo
                         a = A[fb].reshape(4, 16, 8)  # [g4][row][k]
