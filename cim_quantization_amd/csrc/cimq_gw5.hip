@@ -39,6 +39,9 @@ struct G5 {
 };
 
 #ifdef CIMQ_TU_GW5
+// SS: the conv stride (1, or 2 in the tuning build): a compile-time constant, so the pixel-pair offsets
+// stay immediates
+template <int SS>
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
                         const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
@@ -133,7 +136,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       // (W a power of two; the divisions by RH and CH as exact float-reciprocal quotients; 32-bit offsets:
       // g5_plan bounds Nin)
       const int n = 16 * CH * g.W;
-      const int ih0 = oh0 * g.SH - 1;  // patch row 0 (pad 1)
+      const int ih0 = oh0 * SS - 1;  // patch row 0 (pad 1)
       const int xb = (b0 * g.C + 16 * cb) * HWi + ih0 * g.W;  // (image b0, channel 16 cb, row ih0)
       for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
         uint32_t wv[4];
@@ -178,7 +181,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
       const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
       const int pin = pin0 + e0;  // within the image slot
-      const int poff = (sl * v.RH + (pin >> v.lwo) * g.SH) * v.WP + (pin & (Wo - 1)) * g.SW;
+      const int poff = (sl * v.RH + (pin >> v.lwo) * SS) * v.WP + (pin & (Wo - 1)) * SS;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if (q >= ntl) break;
@@ -217,7 +220,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
         for (int fb = 0; fb < 9; ++fb) {
           if (atl[fb] != q) continue;  // uniform: the 16-row blocks of this tile
-          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + g.SW];
+          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + SS];
           const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);

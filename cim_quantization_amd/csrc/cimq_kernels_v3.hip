@@ -621,6 +621,7 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
                 if (CST == 8 && j + k >= 8) {  // mask-0 pair of the wrapped 8-bit mask: zero state bits
 #pragma unroll
                   for (int r = 0; r < 4; ++r) {
+                    if constexpr (!WST) continue;
                     if constexpr (PLF) {
                       const int wd = kj >= 32 ? 1 : 0;
                       sw3[ob][r][wd] <<= 1;
@@ -651,9 +652,10 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
 #endif
                   const uint64_t mhi = __builtin_amdgcn_ballot_w64(ps[j][r] >= pv.x);
                   const uint64_t mlo = __builtin_amdgcn_ballot_w64(ps[j][r] <= pv.y);
+                  acc[ob][r] += adc3(cf, mhi, mlo);
+                  if constexpr (!WST) continue;  // (CSTA 9: no state words -- and none of their bits)
                   const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(ps[j][r] - pv.z) <= (unsigned)pv.w);
                   const uint64_t mnz = mhi | mlo;
-                  acc[ob][r] += adc3(cf, mhi, mlo);
                   if constexpr (PLF) {
                     const int wd = kj >= 32 ? 1 : 0;
                     sw3[ob][r][wd] = shin(sw3[ob][r][wd], mps);

@@ -10,7 +10,7 @@ int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* g
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   if (W.nchunks_bwd != p.v.nchunks) return fail(CIMQ_EINVAL, "internal: cim_bwd_gw5 slab count mismatch");
-  auto kern = cim_bwd_gw5_kernel;
+  auto kern = g.SH == 2 ? cim_bwd_gw5_kernel<2> : cim_bwd_gw5_kernel<1>;
   CIMQ_TRY(set_lds(kern, p.lds));
   const int slot = prof_begin(KID_GW_V7, g, s);
   G5 v = p.v;
