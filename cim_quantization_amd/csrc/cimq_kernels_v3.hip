@@ -609,10 +609,13 @@ __global__ __launch_bounds__(256) void cim_fwd_v3_kernel(Geo g, V3 v, const uint
               v4i ps[NS];
 #pragma unroll
               for (int j = 0; j < NS; ++j) {
-                ps[j] = v4i{0, 0, 0, 0};
                 if (CST != 8 || j + k < 8) {  // compile time once unrolled (w8a8: standard mask only)
+                  // (the first K-step from the inline zero accumulator: no register clearing)
+                  ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][0], wk[0], v4i{0, 0, 0, 0}, 0, 0, 0);
 #pragma unroll
-                  for (int ks = 0; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+                  for (int ks = 1; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+                } else {
+                  ps[j] = v4i{0, 0, 0, 0};  // (a mask-0 pair: never read)
                 }
               }
 #pragma unroll
