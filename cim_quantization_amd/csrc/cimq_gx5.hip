@@ -70,6 +70,7 @@ __global__ void prep_wg5_kernel(Geo g, const float* __restrict__ w_q, const floa
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) wg5_item(g, ws, wg5, t);
 }
 
+template <int CBN>  // 16-channel input blocks = output halves (X5::CBN)
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 8)))
 void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i* __restrict__ wg5, Params pp,
                         const float* __restrict__ sw_p, const float* __restrict__ sa_p,
@@ -82,7 +83,8 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int WP = g.W + 2;
   const int PLANE = 6 * WP * 96;                        // bytes per plane
   const int OW5 = 3 * PLANE + 32;                       // weight operand offset
-  const int NW5 = 9 * 2 * v.CBN * 64;                   // weight fragments per (tile, half)
+  constexpr int NW5 = 9 * 2 * CBN * 64;                 // weight fragments per (tile, half)
+  constexpr int NWI = (NW5 + 511) / 512;                // ... per thread
   float* cel = reinterpret_cast<float*>(smem + OW5 + NW5 * 16);  // cE_kj
   float* red = cel + 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -126,7 +128,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
         const int oh = r0 - 1 + row;
 #pragma unroll
         for (int e = 0; e < 4; ++e) gvr[hh][k][e] = 0.f;
-        if (hh < v.CBN && it < NG && (unsigned)oh < (unsigned)g.Ho) {
+        if (hh < CBN && it < NG && (unsigned)oh < (unsigned)g.Ho) {
           const int pimg = oh * g.Wo + col;
           const int go = g.onchw ? (b * g.O + 4 * oq) * g.P + pimg : (b * g.P + pimg) * g.O + 4 * oq;
 #pragma unroll
@@ -136,12 +138,35 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
     for (int i = 0; i < g.T; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (h >= v.CBN) break;
-      const int ih2 = i * v.CBN + h;  // step: tile i, output half h
+      if (h >= CBN) break;
+      const int ih2 = i * CBN + h;  // step: tile i, output half h
+      // the step's global reads, all issued before the barrier and the first wait: its weight operand and
+      // the state words of its G-patch items (a copy loop and then the build's loads were 2-4 dependent
+      // round trips per step)
+      v4i wv[NWI];
+#pragma unroll
+      for (int u = 0; u < NWI; ++u) {
+        const int idx = threadIdx.x + u * 512;
+        if (idx < NW5) wv[u] = wg5[ih2 * NW5 + idx];
+      }
+      uint4 s4r[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int it = threadIdx.x + kk * 512;
+        const int rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
+        const int oh = r0 - 1 + row;
+        s4r[kk] = make_uint4(0u, 0u, 0u, 0u);
+        if (it < NG && (unsigned)oh < (unsigned)g.Ho) {
+          const int m = b * g.P + oh * g.Wo + col;
+          s4r[kk] = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * ((it & 3) + 4 * h)));
+        }
+      }
       __syncthreads();  // the previous step's (or m-tile's) MFMAs are done with the patch and weights
-      // the step's weight operand
-      batched_copy<2>(NW5, reinterpret_cast<v4i*>(smem + OW5),
-                      [&](int idx) -> v4i { return wg5[(size_t)ih2 * NW5 + idx]; });
+#pragma unroll
+      for (int u = 0; u < NWI; ++u) {
+        const int idx = threadIdx.x + u * 512;
+        if (idx < NW5) reinterpret_cast<v4i*>(smem + OW5)[idx] = wv[u];
+      }
       // G patch of output rows r0 - 1 .. r0 + 4, output channels 16 h .. 16 h + 15: item = (row, col,
       // 4 channels), channels fastest
       // (32-bit offsets -- x5_plan bounds T * M * O -- W a power of two, the grad_out layout's element stride
@@ -153,13 +178,8 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const int it = threadIdx.x + kk * (int)blockDim.x;
           if (it >= NG) continue;
           const int oq = (it & 3) + 4 * h, rc = it >> 2, col = rc & (g.W - 1), row = rc >> v.lw;
-          const int oh = r0 - 1 + row;
           const float* gv = gvr[h][kk];
-          uint4 s4 = make_uint4(0u, 0u, 0u, 0u);
-          if ((unsigned)oh < (unsigned)g.Ho) {
-            const int m = b * g.P + oh * g.Wo + col;
-            s4 = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * oq));
-          }
+          const uint4 s4 = s4r[kk];
           const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
           uint8_t* px = smem + (row * WP + col + 1) * 96 + 8 * (oq - 4 * h);
 #pragma unroll
@@ -204,7 +224,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const v8bf ah = as_v8bf(*reinterpret_cast<const v4i*>(pa + 64 * s));
           const v8bf am = as_v8bf(*reinterpret_cast<const v4i*>(pa + PLANE + 64 * s));
           const v8bf al = as_v8bf(*reinterpret_cast<const v4i*>(pa + 2 * PLANE + 64 * s));
-          const v8bf w = as_v8bf(wb[(p * 2 + s) * v.CBN * 64]);
+          const v8bf w = as_v8bf(wb[(p * 2 + s) * CBN * 64]);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w, acc, 0, 0, 0);

@@ -10,7 +10,7 @@ int launch_gx5(const Geo& g, const PlanX5& p, const uint8_t* ctx, const float* s
   if (!p.ok) return fail(CIMQ_EINVAL, "internal: cim_bwd_gx5 off its plan");
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
-  auto kern = cim_bwd_gx5_kernel;
+  auto kern = p.v.CBN == 2 ? cim_bwd_gx5_kernel<2> : cim_bwd_gx5_kernel<1>;
   CIMQ_TRY(set_lds(kern, p.lds));
   const int slot = prof_begin(KID_GX_V8, g, s);
   hipLaunchKernelGGL(kern, dim3(p.nblk), dim3(512), p.lds, s, g, p.v, reinterpret_cast<const uint32_t*>(ctx + L.st),
