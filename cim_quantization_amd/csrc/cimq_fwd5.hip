@@ -214,68 +214,78 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
     for (int q = 0; q < v.ngrp; ++q) {
       const int cb0 = v.gcb0[q], ncb = v.gcb1[q] - cb0 + 1;
       const int QC = ncb * 4;  // staged 4-channel groups
-      __syncthreads();  // the previous group's / m-tile's waves are done with the patch (and the fragments)
-      if (v.ngrp > 1) stage_b(q);
-      {
-        // row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32
-        // loads); quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices
-        // into the slice planes, store the ctx words of owned rows and channel blocks
-        // (index arithmetic in 32 bits -- f5_plan bounds Nin -- with the divisions by the runtime QC and RH
-        // as exact float-reciprocal quotients, and every item's decomposition computed once)
-        const int n = v.IPM * v.RH * QC * g.W;
-        const float invQC = 1.f / (float)QC, invRH = 1.f / (float)v.RH;
-        const int xbase = (b0 * g.C + 16 * cb0) * HWi + ih0 * g.W;  // element (image b0, channel 16 cb0, row ih0, col 0)
-        for (int base = threadIdx.x; base < n; base += 2 * (int)blockDim.x) {
-          float xv[2][4];
-          int dsto[2], xo[2], ihs[2], qqs[2];
+      // row staging: item = (image slot, row, 4-channel group, col), col fastest (coalesced fp32 loads);
+      // quantise (act_words_tab: the prologue's own table), transpose 4 channels x 3 slices into the slice
+      // planes, store the ctx words of owned rows and channel blocks.  SU items per thread and round; the
+      // first round's reads are issued before the barrier (every stride-1 layer stages in that one round)
+      // (index arithmetic in 32 bits -- f5_plan bounds Nin -- with the divisions by the runtime QC and RH
+      // as exact float-reciprocal quotients, and every item's decomposition computed once)
+      constexpr int SU = NOB == 2 ? 3 : 2;
+      constexpr int NT = 512 * NOB;
+      const int n = v.IPM * v.RH * QC * g.W;
+      const float invQC = 1.f / (float)QC, invRH = 1.f / (float)v.RH;
+      const int xbase = (b0 * g.C + 16 * cb0) * HWi + ih0 * g.W;  // element (image b0, channel 16 cb0, row ih0, col 0)
+      float xv[SU][4];
+      int dsto[SU], xo[SU], ihs[SU], qqs[SU];
+      auto ldx = [&](int base) {
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int idx = base + u * (int)blockDim.x;
-            dsto[u] = -1;
+        for (int u = 0; u < SU; ++u) {
+          const int idx = base + u * NT;
+          dsto[u] = -1;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
-            if (idx < n) {
-              const int col = idx & (g.W - 1), r1 = idx >> v.lwi;
-              const int r2 = sdiv(r1, invQC), qq = r1 - r2 * QC;
-              const int sl = sdiv(r2, invRH), row = r2 - sl * v.RH;
-              ihs[u] = ih0 + row;
-              qqs[u] = qq;
-              dsto[u] = sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) + 4 * (qq & 3);
-              xo[u] = xbase + (sl * g.C + 4 * qq) * HWi + row * g.W + col;
-              if ((unsigned)ihs[u] < (unsigned)g.H) {
+          for (int e = 0; e < 4; ++e) xv[u][e] = 0.f;
+          if (idx < n) {
+            const int col = idx & (g.W - 1), r1 = idx >> v.lwi;
+            const int r2 = sdiv(r1, invQC), qq = r1 - r2 * QC;
+            const int sl = sdiv(r2, invRH), row = r2 - sl * v.RH;
+            ihs[u] = ih0 + row;
+            qqs[u] = qq;
+            dsto[u] = sl * IMGB + f5_off(v.NCBP, v.WP, row, qq >> 2, col + 1) + 4 * (qq & 3);
+            xo[u] = xbase + (sl * g.C + 4 * qq) * HWi + row * g.W + col;
+            if ((unsigned)ihs[u] < (unsigned)g.H) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) xv[u][e] = x[xo[u] + e * HWi];
-              }
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            if (dsto[u] < 0) continue;
-            uint32_t* dst = reinterpret_cast<uint32_t*>(patch + dsto[u]);
-            const int ih = ihs[u];
-            if ((unsigned)ih >= (unsigned)g.H) {
-              dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
-              continue;
-            }
-            uint2 w[4];
-            int code[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut, code[e]);
-            uint32_t P[4];
-            tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
-            dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
-            if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
-              if (v.codes) {  // one byte per element: grad_w expands it through the same word table
-                uint8_t* cb8 = reinterpret_cast<uint8_t*>(xcb);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) cb8[xo[u] + e * HWi] = (uint8_t)code[e];
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
-              }
+              for (int e = 0; e < 4; ++e) xv[u][e] = x[xo[u] + e * HWi];
             }
           }
         }
+      };
+      auto stx = [&]() {
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          if (dsto[u] < 0) continue;
+          uint32_t* dst = reinterpret_cast<uint32_t*>(patch + dsto[u]);
+          const int ih = ihs[u];
+          if ((unsigned)ih >= (unsigned)g.H) {
+            dst[0] = 0u; dst[4] = 0u; dst[8] = 0u;
+            continue;
+          }
+          uint2 w[4];
+          int code[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = act_words_q5(xv[u][e], sa, nan_e - 1, nan_e, alut, code[e]);
+          uint32_t P[4];
+          tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
+          dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
+          if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
+            if (v.codes) {  // one byte per element: grad_w expands it through the same word table
+              uint8_t* cb8 = reinterpret_cast<uint8_t*>(xcb);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) cb8[xo[u] + e * HWi] = (uint8_t)code[e];
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) xcb[xo[u] + e * HWi] = w[e].y;
+            }
+          }
+        }
+      };
+      // (one instance of each phase: the first round, which every thread runs, holds the barrier)
+      for (int base = (int)threadIdx.x, first = 1; first || base < n; base += SU * NT, first = 0) {
+        ldx(base);
+        if (first) {
+          __syncthreads();  // the previous group's / m-tile's waves are done with the patch (and the fragments)
+          if (v.ngrp > 1) stage_b(q);
+        }
+        stx();
       }
       __syncthreads();
 

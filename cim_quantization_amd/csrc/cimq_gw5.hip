@@ -26,6 +26,9 @@ namespace cimq {
 // n / d for 0 <= n < 2^20, d < 2^10 (inv = 1 / d in fp32): exact
 __device__ inline int sdiv5(int n, float inv) { return (int)(((float)n + 0.5f) * inv); }
 
+// the code -> ctx word table's entry for out-of-image elements (a zero word; codes are <= 256)
+constexpr int kZeroCode = 259;
+
 struct G5 {
   int lwo;     // log2(Wo)
   int lwi;     // log2(W)
@@ -41,7 +44,7 @@ struct G5 {
 #ifdef CIMQ_TU_GW5
 // SS: the conv stride (1, or 2 in the tuning build): a compile-time constant, so the pixel-pair offsets
 // stay immediates
-template <int SS>
+template <int SS, bool CODES>  // CODES: G5::codes, a compile-time choice of the staging's load width
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
                         const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
@@ -62,9 +65,12 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int ntl = i_hi - i_lo + 1;
   for (int t = threadIdx.x; t < 9; t += blockDim.x) cdl[t] = pp.ckj[18 + t];
   // the forward's backward-word table (ctx, written by cim_fwd5_kernel): code e -> ctx word
-  if (v.codes)
+  // (entry kZeroCode: 0, the code of the staging's out-of-image elements)
+  if (CODES) {
     for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x)
       *reinterpret_cast<uint32_t*>(smem + alut_off + 4 * t) = cal[t];
+    if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + alut_off + 4 * kZeroCode) = 0u;
+  }
   // padding columns 0 and WP-1: zero once
   for (int t = threadIdx.x; t < 16 * CH * 2; t += blockDim.x) {
     const int side = t & 1, cr = t >> 1;
@@ -82,11 +88,14 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 
   // per 16-row block fb: this lane's row f = 144 cb + 16 fb + r16 = (c, kh, kw) -> patch offset (uint2
   // units, c relative to the block), and its tile (slot 0 or 1 of the block's tiles)
-  int aoff[9], atl[9];
+  // (two 16-bit offsets per register, unpacked per use: g5_plan's one-round staging bound keeps the patch
+  // below 2^16 uint2)
+  uint32_t aoffp[5] = {0u, 0u, 0u, 0u, 0u};
+  int atl[9];
 #pragma unroll
   for (int fb = 0; fb < 9; ++fb) {
     const int f = 16 * fb + r16, c = f / 9, p = f - 9 * c, kh = p / 3, kw = p - 3 * kh;
-    aoff[fb] = (c * CH + kh) * v.WP + kw;
+    aoffp[fb >> 1] |= (uint32_t)((c * CH + kh) * v.WP + kw) << (16 * (fb & 1));
     atl[fb] = (144 * cb + 16 * fb) / 128 - i_lo;  // uniform
   }
   v4f acc[9];
@@ -105,6 +114,8 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int tpi = g.P >= 128 ? g.P / 128 : 1;
   const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
   for (int mt = mt_lo; mt < mt_hi; ++mt) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) asm volatile("" : "+v"(aoffp[k]));
     const int b0 = g.P >= 128 ? mt / tpi : mt * v.IPM;  // first image of the m-tile
     const int p0 = g.P >= 128 ? (mt - b0 * tpi) * 128 : 0;
     const int oh0 = p0 >> v.lwo;
@@ -128,51 +139,52 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
         for (int e = 0; e < 4; ++e) sq[q][e] = q < ntl ? st[((size_t)(i_lo + q) * g.M + m + e) * g.O + o] : 0u;
     }
-    __syncthreads();  // the previous m-tile's waves are done with the patch
-    {
-      // A-ready patch: input rows oh0 * SH - 1 .. (oh0 + R - 1) * SH + 1 of each image slot, the block's 16
-      // channels; item =
-      // (c, slot, row, col)
-      // (W a power of two; the divisions by RH and CH as exact float-reciprocal quotients; 32-bit offsets:
-      // g5_plan bounds Nin)
-      const int n = 16 * CH * g.W;
-      const int ih0 = oh0 * SS - 1;  // patch row 0 (pad 1)
-      const int xb = (b0 * g.C + 16 * cb) * HWi + ih0 * g.W;  // (image b0, channel 16 cb, row ih0)
-      for (int base = threadIdx.x; base < n; base += 4 * (int)blockDim.x) {
-        uint32_t wv[4];
-        int dst[4];
-        bool inb[4];
+    // A-ready patch: input rows oh0 * SH - 1 .. (oh0 + R - 1) * SH + 1 of each image slot, the block's 16
+    // channels; item = (c, slot, row, col) (W a power of two; the divisions by RH and CH as exact
+    // float-reciprocal quotients; 32-bit offsets: g5_plan bounds Nin).  SU items per thread: their
+    // reads are issued with grad_out's and the state words', before the barrier (one round:
+    // g5_plan checks 16 * CH * W <= SU * 512)
+    constexpr int SU = 6;
+    const int n = 16 * CH * g.W;
+    const int ih0 = oh0 * SS - 1;  // patch row 0 (pad 1)
+    const int xb = (b0 * g.C + 16 * cb) * HWi + ih0 * g.W;  // (image b0, channel 16 cb, row ih0)
+    auto ld = [&](int base, uint32_t (&wv)[SU]) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int idx = base + u * (int)blockDim.x;
-          dst[u] = -1;
-          wv[u] = 0u;
-          inb[u] = false;
-          if (idx < n) {
-            const int col = idx & (g.W - 1), cr = idx >> v.lwi;
-            const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
-            const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
-            const int ih = ih0 + row;
-            dst[u] = cr * v.WP + col + 1;
-            if ((unsigned)ih < (unsigned)g.H) {
-              inb[u] = true;
-              const int xi = xb + (slt * g.C + c) * HWi + row * g.W + col;
-              // (a code byte, expanded below through the LDS table, or the word itself)
-              wv[u] = v.codes ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[xi] : xcb[xi];
-            }
+      for (int u = 0; u < SU; ++u) {
+        const int idx = base + u * 512;
+        wv[u] = CODES ? kZeroCode : 0u;
+        if (idx < n) {
+          const int col = idx & (g.W - 1), cr = idx >> v.lwi;
+          const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
+          const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
+          const int ih = ih0 + row;
+          if ((unsigned)ih < (unsigned)g.H) {
+            const int xi = xb + (slt * g.C + c) * HWi + row * g.W + col;
+            // (a code byte, expanded below through the LDS table, or the word itself)
+            // (unsigned offsets: the loads take the scalar base + 32-bit offset form)
+            wv[u] = CODES ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[(uint32_t)xi] : xcb[(uint32_t)xi];
           }
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (dst[u] < 0) continue;
-          if (v.codes && inb[u]) wv[u] = *reinterpret_cast<const uint32_t*>(smem + alut_off + 4 * (int)wv[u]);
-          // int8 ctx slices (lsq.py:160 truncation, wrapped) -> exact bf16 (the high half of the fp32)
-          const uint32_t f0 = __float_as_uint((float)(int8_t)(wv[u] & 0xFFu));
-          const uint32_t f1 = __float_as_uint((float)(int8_t)((wv[u] >> 8) & 0xFFu));
-          const uint32_t f2 = __float_as_uint((float)(int8_t)((wv[u] >> 16) & 0xFFu));
-          pat[dst[u]] = make_uint2(__builtin_amdgcn_perm(f1, f0, 0x07060302u), f2 >> 16);
-        }
       }
+    };
+    auto stv = [&](int base, uint32_t (&wv)[SU]) {
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int idx = base + u * 512;
+        if (idx >= n) continue;
+        if (CODES) wv[u] = *reinterpret_cast<const uint32_t*>(smem + alut_off + 4 * (int)wv[u]);
+        // int8 ctx slices (lsq.py:160 truncation, wrapped) -> exact bf16 (the high half of the fp32)
+        const uint32_t f0 = __float_as_uint((float)(int8_t)(wv[u] & 0xFFu));
+        const uint32_t f1 = __float_as_uint((float)(int8_t)((wv[u] >> 8) & 0xFFu));
+        const uint32_t f2 = __float_as_uint((float)(int8_t)((wv[u] >> 16) & 0xFFu));
+        pat[(idx >> v.lwi) * v.WP + (idx & (g.W - 1)) + 1] = make_uint2(__builtin_amdgcn_perm(f1, f0, 0x07060302u), f2 >> 16);
+      }
+    };
+    {
+      uint32_t wv[SU];
+      ld((int)threadIdx.x, wv);
+      __syncthreads();  // the previous m-tile's waves are done with the patch
+      stv((int)threadIdx.x, wv);
     }
     __syncthreads();
 
@@ -220,7 +232,8 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
         for (int fb = 0; fb < 9; ++fb) {
           if (atl[fb] != q) continue;  // uniform: the 16-row blocks of this tile
-          const uint2 a0 = pat[aoff[fb] + poff], a1 = pat[aoff[fb] + poff + SS];
+          const int ao = (int)((aoffp[fb >> 1] >> (16 * (fb & 1))) & 0xFFFFu);
+          const uint2 a0 = pat[ao + poff], a1 = pat[ao + poff + SS];
           const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);

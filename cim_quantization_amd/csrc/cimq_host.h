@@ -818,6 +818,9 @@ inline PlanG5 g5_plan(const Geo& g) {
   v.R = std::min(g.P, 128) / g.Wo;
   v.RH = (v.R - 1) * g.SH + 3;
   v.WP = g.W + 2;
+  // the kernel stages an m-tile's patch in one round of six items per thread, its reads issued before the
+  // barrier (the stride-1 16 / 32-channel layers: 3072 / 2560 items; stride 2 stages 17 rows, beyond it)
+  if (16 * v.IPM * v.RH * g.W > 6 * 512) return p;
   v.nmt = g.M / 128;
   p.pairs = (g.C / 16) * g.OB16;
   // blocks: about two per CU; chunks (slabs) = blocks / pairs

@@ -10,11 +10,12 @@ int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* g
   CtxLayout L = ctx_layout(g);
   WsLayout W = ws_layout(g);
   if (W.nchunks_bwd != p.v.nchunks) return fail(CIMQ_EINVAL, "internal: cim_bwd_gw5 slab count mismatch");
-  auto kern = g.SH == 2 ? cim_bwd_gw5_kernel<2> : cim_bwd_gw5_kernel<1>;
-  CIMQ_TRY(set_lds(kern, p.lds));
-  const int slot = prof_begin(KID_GW_V7, g, s);
   G5 v = p.v;
   v.codes = ctx_codes(g) ? 1 : 0;  // the forward wrote code bytes (cim_fwd5_kernel on the module path)
+  auto kern = g.SH == 2 ? (v.codes ? cim_bwd_gw5_kernel<2, true> : cim_bwd_gw5_kernel<2, false>)
+                        : (v.codes ? cim_bwd_gw5_kernel<1, true> : cim_bwd_gw5_kernel<1, false>);
+  CIMQ_TRY(set_lds(kern, p.lds));
+  const int slot = prof_begin(KID_GW_V7, g, s);
   hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(512), p.lds, s, g, v,
                      reinterpret_cast<const uint32_t*>(ctx + L.st), reinterpret_cast<const uint32_t*>(ctx + L.xhat),
                      params_of(g, const_cast<uint8_t*>(ctx)), gout, reinterpret_cast<const uint32_t*>(ctx + L.alut),
