@@ -228,6 +228,21 @@ __device__ inline void gw_lsq_role(const Geo& g, const LsqArgs& q, const ModuleT
     return;
   }
   if (!a.wide) {  // nout % 16 == 0 (Opad)
+    {
+      // a block whose rows are all padding rows of one tile (rows xbar .. FBT*16 - 1 of a tile, or past K
+      // in the last one: gw_pre's e = -1) has nothing to sum: its slab reads skipped (the 16-channel layers'
+      // second tile holds 16 rows of 128)
+      const size_t r0 = (size_t)blk * a.lpr * 4 / g.Opad, r1 = ((size_t)(blk + 1) * a.lpr * 4 - 1) / g.Opad;
+      const size_t tr = (size_t)g.FBT * 16;
+      const int i = (int)(r0 / tr), fl = (int)(r0 - (size_t)i * tr);
+      if (r1 / tr == (size_t)i && (fl >= g.xbar || i * g.xbar + fl >= g.K)) {
+        if (threadIdx.x == 0) {
+          a.wpart[2 * blk] = 0.f;
+          a.wpart[2 * blk + 1] = 0.f;
+        }
+        return;
+      }
+    }
     const size_t i0 = ((size_t)blk * a.lpr + (threadIdx.x & (a.lpr - 1))) * 4;
     const bool mine = (int)threadIdx.x < a.lpr && i0 < nout;
     GwPre pre[4];
