@@ -405,7 +405,9 @@ inline Plan7 v7_plan(const Geo& g) {
   else if (128 % g.P == 0) v.whole = 1;
   else return p;
   v.lw = p3.v.lw;
-  v.RB = std::min(g.H, tune("GX_RB", 8));
+  // input rows per band: 16 (round 5, once only the stride-2 layers of the benchmark still ran this kernel:
+  // 105.7 -> 80.6 us/step for ResNet-20's two; 8 and 32 slower, gpurun_out/r05_sw7, r05_sw8)
+  v.RB = std::min(g.H, tune("GX_RB", 16));
   v.nbands = (g.H + v.RB - 1) / v.RB;
   v.FBX = g.FBT;
   // grad_x v8: (c, kh)-row blocks per tile, ring of output rows
