@@ -42,8 +42,7 @@ struct G5 {
 };
 
 #ifdef CIMQ_TU_GW5
-// SS: the conv stride (1, or 2 in the tuning build): a compile-time constant, so the pixel-pair offsets
-// stay immediates
+// SS: the conv stride (1 or 2): a compile-time constant, so the pixel-pair offsets stay immediates
 template <int SS, bool CODES>  // CODES: G5::codes, a compile-time choice of the staging's load width
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
@@ -141,9 +140,9 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     }
     // A-ready patch: input rows oh0 * SH - 1 .. (oh0 + R - 1) * SH + 1 of each image slot, the block's 16
     // channels; item = (c, slot, row, col) (W a power of two; the divisions by RH and CH as exact
-    // float-reciprocal quotients; 32-bit offsets: g5_plan bounds Nin).  SU items per thread: their
-    // reads are issued with grad_out's and the state words', before the barrier (one round:
-    // g5_plan checks 16 * CH * W <= SU * 512)
+    // float-reciprocal quotients; 32-bit offsets: g5_plan bounds Nin).  SU items per thread and round: the
+    // first round's reads are issued with grad_out's and the state words', before the barrier (the stride-1
+    // layers stage in that one round)
     constexpr int SU = 6;
     const int n = 16 * CH * g.W;
     const int ih0 = oh0 * SS - 1;  // patch row 0 (pad 1)
@@ -180,11 +179,18 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
         pat[(idx >> v.lwi) * v.WP + (idx & (g.W - 1)) + 1] = make_uint2(__builtin_amdgcn_perm(f1, f0, 0x07060302u), f2 >> 16);
       }
     };
-    {
+    if constexpr (SS == 1) {  // one round (g5_plan: 16 * CH * W <= SU * 512 at stride 1)
       uint32_t wv[SU];
       ld((int)threadIdx.x, wv);
       __syncthreads();  // the previous m-tile's waves are done with the patch
       stv((int)threadIdx.x, wv);
+    } else {  // stride 2: further rounds after the barrier
+      for (int base = (int)threadIdx.x, first = 1; first || base < n; base += SU * 512, first = 0) {
+        uint32_t wv[SU];
+        ld(base, wv);
+        if (first) __syncthreads();
+        stv(base, wv);
+      }
     }
     __syncthreads();
 

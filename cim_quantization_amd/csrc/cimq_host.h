@@ -801,9 +801,10 @@ inline PlanG5 g5_plan(const Geo& g) {
       g.xbar != 128)
     return p;
   if (g.W != g.Wo * g.SH || g.H != g.Ho * g.SH) return p;  // (stride 2: even input sides)
-  // stride 2 measured slower than cim_bwd_gw_v7_kernel (51.5 vs 43 us per launch on ResNet-20's two
-  // transition layers: 17 staged rows for 8 output rows); kept for the tuning build
-  if (g.SH == 2 && tune("GW5_S2", 0) == 0) return p;
+  // stride 2 (17 staged rows for 8 output rows): 65.8 vs cim_bwd_gw_v7_kernel's 87.4 us/step on ResNet-20's
+  // two transition layers once the staging's first round went before the barrier (51.5 vs 43 us per
+  // launch before: gpurun_out/r05_sw11)
+  if (g.SH == 2 && tune("GW5_S2", 1) == 0) return p;
   if (g.C % 16 != 0 || g.O % 16 != 0 || g.Wo % 4 != 0) return p;
   if (g.P >= 128 ? g.P % 128 != 0 : (128 % g.P != 0 || g.P % 16 != 0)) return p;
   if (g.M % 128 != 0) return p;  // whole 128-pixel m-tiles
@@ -820,9 +821,11 @@ inline PlanG5 g5_plan(const Geo& g) {
   v.R = std::min(g.P, 128) / g.Wo;
   v.RH = (v.R - 1) * g.SH + 3;
   v.WP = g.W + 2;
-  // the kernel stages an m-tile's patch in one round of six items per thread, its reads issued before the
-  // barrier (the stride-1 16 / 32-channel layers: 3072 / 2560 items; stride 2 stages 17 rows, beyond it)
-  if (16 * v.IPM * v.RH * g.W > 6 * 512) return p;
+  // the kernel stages an m-tile's patch in rounds of six items per thread, the first round's reads issued
+  // before the barrier (the stride-1 16 / 32-channel layers: 3072 / 2560 items, one round; stride 2 stages
+  // 17 rows, three rounds); the packed row offsets need the patch below 2^16 uint2
+  if ((long long)16 * v.IPM * v.RH * v.WP >= (1LL << 16)) return p;
+  if (g.SH == 1 && 16 * v.IPM * v.RH * g.W > 6 * 512) return p;
   v.nmt = g.M / 128;
   p.pairs = (g.C / 16) * g.OB16;
   // blocks: about two per CU; chunks (slabs) = blocks / pairs

@@ -182,9 +182,9 @@ def test_module_route_resnet20(lib):
     want = {
         "conv1": ("v3", "c1", "c1"),
         "layer1.0.conv1": ("fwd5", "gx5", "gw5"),
-        "layer2.0.conv1": ("fwd5", "v7", "v7"),   # stride 2: the v8 / v7 pair
+        "layer2.0.conv1": ("fwd5", "v7", "gw5"),  # stride 2: gx_v8, and gw5 at stride 2
         "layer2.0.conv2": ("fwd5", "gx5", "gw5"),
-        "layer3.0.conv1": ("fwd5", "v7", "v7"),   # stride 2: fwd5 with two output blocks per workgroup (its larger LDS budget)
+        "layer3.0.conv1": ("fwd5", "v7", "gw5"),  # stride 2: fwd5 with two output blocks per workgroup (its larger LDS budget)
         "layer3.0.conv2": ("fwd5", "fused", "fused"),
     }
     code = {0: "general", 1: "v3", 2: "fwd5", 3: "v7", 4: "fused", 5: "c1", 6: "gx5", 7: "gw5", 8: "dense"}  # CIMQ_ROUTE_*
