@@ -13,13 +13,16 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 CIMQ_EINVAL = 1  # include/cimq.h error codes
 CIMQ_EUNSUPPORTED = 2
 CIMQ_EHIP = 3
 CIMQ_INPUT_XQ = 0
 CIMQ_INPUT_RAW_LSQ = 1
+# cimq_module_route codes (include/cimq.h CIMQ_ROUTE_*)
+ROUTE_NAMES = {0: "general", 1: "v3", 2: "fwd5", 3: "v7", 4: "fused", 5: "c1", 6: "gx5", 7: "gw5", 8: "dense", 9: "r6"}
+CIMQ_ROUTE_R6 = 9
 CIMQ_LSQ_ACCUMULATE_GRADS = 1
 CIMQ_LSQ_SKIP_TAIL = 2
 CIMQ_LSQ_DEFER_GW = 4
@@ -55,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "cimq_shift_backward",
     "cimq_debug_partial_sums",
     "cimq_debug_state_codes",
+    "cimq_debug_recompute_codes",
     "cimq_lsq_quantize_forward",
     "cimq_lsq_quantize_workspace_bytes",
     "cimq_lsq_quantize_backward",
@@ -129,7 +133,8 @@ class Sizes(ctypes.Structure):
     """Mirror of ``cimq_sizes``."""
 
     _fields_ = [("ctx_bytes", ctypes.c_size_t), ("fwd_workspace_bytes", ctypes.c_size_t),
-                ("bwd_workspace_bytes", ctypes.c_size_t), ("wprep_bytes", ctypes.c_size_t)]
+                ("bwd_workspace_bytes", ctypes.c_size_t), ("wprep_bytes", ctypes.c_size_t),
+                ("module_ctx_bytes", ctypes.c_size_t)]
 
 
 class PrepareItem(ctypes.Structure):
@@ -195,6 +200,8 @@ def _bind(lib):
     lib.cimq_debug_partial_sums.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 12
     lib.cimq_debug_state_codes.restype = ctypes.c_int
     lib.cimq_debug_state_codes.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 4
+    lib.cimq_debug_recompute_codes.restype = ctypes.c_int
+    lib.cimq_debug_recompute_codes.argtypes = [ctypes.POINTER(ConvDesc)] + [_VP] * 7
     _F, _LL, _I = ctypes.c_float, ctypes.c_longlong, ctypes.c_int
     lib.cimq_lsq_quantize_forward.restype = ctypes.c_int
     lib.cimq_lsq_quantize_forward.argtypes = [_VP, _LL, _VP, _F, _F, _I, _VP, _VP]
@@ -294,6 +301,13 @@ def qconv_sizes(desc: QConvDesc):
     f, b = ctypes.c_size_t(), ctypes.c_size_t()
     check(load().cimq_qconv_sizes(ctypes.byref(desc), ctypes.byref(f), ctypes.byref(b)), "cimq_qconv_sizes")
     return f.value, b.value
+
+
+def module_route(desc: ConvDesc):
+    """(forward, grad_x, grad_w) CIMQ_ROUTE_* codes of the module entry points for ``desc``."""
+    r = (ctypes.c_int * 3)()
+    check(load().cimq_module_route(ctypes.byref(desc), r), "cimq_module_route")
+    return tuple(r)
 
 
 def query_sizes(desc: ConvDesc) -> Sizes:

@@ -64,7 +64,7 @@ int prep_all(const Geo& g, const float* x, const float* w_q, const float* sa, co
 // kernel leaves cimq_module_backward for cimq_module_backward_params (the fused / first-conv kernels
 // and the general paths produce both in one pass)
 static bool gw_deferrable(const Geo& g) {
-  return g.variant == VAR_LIBRARY && v7_bwd(g) && !c1_plan(g).ok && !v9_plan(g).ok;
+  return g.variant == VAR_LIBRARY && v7_bwd(g) && !c1_plan(g).ok && !v9_plan(g).ok && !r6_bwd(g);
 }
 
 // parts: bit 0 grad_x (with everything a single-pass backward produces), bit 1 the deferred grad_w
@@ -79,6 +79,11 @@ int dispatch_bwd_any(const Geo& g, const uint8_t* ctx, const float* sw, const fl
       return launch_dense_bwd(g, ctx, sw, gout, gx, ws, s, *lsq_fused ? x : nullptr, sa);
     }
     return launch_bwd_general(g, ctx, sw, sa, signed_act, gout, x, gx, ws, s, lsq_fused);
+  }
+  if (r6_bwd(g)) {  // the module path's w3a3 16-channel layers: recompute, no state words (cimq_r6.hip)
+    if (!signed_act) return fail(CIMQ_EINVAL, "internal: the recompute backward needs signed_act");
+    *lsq_fused = true;
+    return launch_r6(g, r6_plan(g), ctx, sw, sa, signed_act, gout, x, gx, ws, s);
   }
   const PlanC1 pc = c1_plan(g);
   if (pc.ok) {
@@ -132,7 +137,7 @@ int launch_reduce_slab(const Geo& g, const uint8_t* ctx, uint8_t* ws, size_t sla
 // else one per lsq_act_bwd_kernel block)
 int act_parts(const Geo& g) {
   if (v7_bwd(g)) {
-    if (v9_plan(g).ok || c1_plan(g).ok) return g.B;
+    if (v9_plan(g).ok || c1_plan(g).ok || r6_bwd(g)) return g.B;
     const PlanX5 p5 = x5_plan(g);
     if (p5.ok) return p5.nblk;
     return g.B * v7_plan(g).v.nbands;
@@ -159,6 +164,9 @@ int cimq_query_sizes(const cimq_conv_desc* d, cimq_sizes* out) {
   WsLayout W = ws_layout(g);
   out->fwd_workspace_bytes = W.total;
   out->bwd_workspace_bytes = W.total;
+  Geo gm = g;
+  gm.onchw = 1;  // the module entry points' layout: no state words where their backward recomputes
+  out->module_ctx_bytes = ctx_layout(gm).total;
   return CIMQ_OK;
 }
 
@@ -286,6 +294,24 @@ int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* cod
   const long long n = (long long)g.T * g.M * g.O;
   hipLaunchKernelGGL(decode_state_kernel, dim3(std::min(cdiv(n, 256), 8192)), dim3(256), 0, s, g, g.NBP == 8 ? 1 : 0,
                      c + ctx_layout(g).st, code_out, pass_out);
+  return check_hip("decode_state");
+}
+
+int cimq_debug_recompute_codes(const cimq_conv_desc* d, const float* x, const float* signed_act, const void* ctx,
+                               void* st_scratch, int8_t* code_out, uint8_t* pass_out, void* stream) {
+  Geo g;
+  CIMQ_TRY(make_geo(d, &g));
+  if (!x || !signed_act || !ctx || !st_scratch || !code_out || !pass_out) return fail(CIMQ_EINVAL, "null pointer argument");
+  g.onchw = 1;  // the module entry points' layer
+  if (!r6_bwd(g)) return fail(CIMQ_EUNSUPPORTED, "this layer's module backward does not recompute the partial sums");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
+  const float* scal = reinterpret_cast<const float*>(wreg(g, c) + ctx_layout(g).lsq_scal);
+  uint32_t* st = reinterpret_cast<uint32_t*>(st_scratch);
+  CIMQ_TRY(launch_r6(g, r6_plan(g), c, scal + 1, scal, signed_act, nullptr, x, nullptr, nullptr, s, st));
+  const long long n = (long long)g.T * g.M * g.O;
+  hipLaunchKernelGGL(decode_state_kernel, dim3(std::min(cdiv(n, 256), 8192)), dim3(256), 0, s, g, 0,
+                     reinterpret_cast<const uint8_t*>(st), code_out, pass_out);
   return check_hip("decode_state");
 }
 
@@ -541,8 +567,10 @@ static ModulePrep module_prep_args(const Geo& g, const float* x, const float* we
   a.nw5 = (int)f5_frag_items(g, p5);  // cim_fwd5_kernel's weight operand
   a.wg5 = reinterpret_cast<v4i*>(wr + L.wg5);
   a.nwx5 = (int)(x5_frag_bytes(g) / 16);  // cim_bwd_gx5_kernel's weight operand
+  a.wx6 = reinterpret_cast<v4i*>(wr + L.wx6);
+  a.nwx6 = (int)(r6_frag_bytes(g) / 16);  // cim_bwd_r6_kernel's gx operand
   a.npp = g.T * g.nba * g.nbw * g.Opad + g.nbw * g.nba;
-  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.npp, 256), 1024));
+  *nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.nwx6 + a.npp, 256), 1024));
   return a;
 }
 
@@ -587,7 +615,7 @@ static int module_forward_impl(const cimq_conv_desc* d, const cimq_lsq_desc* q, 
     if (beta_cim) {  // the shift ADC: beta into the thresholds, and the per-channel beta sums
       a.beta = beta_cim;
       a.npp += g.Opad;
-      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.npp, 256), 1024));
+      nwblk = std::max(1, std::min(cdiv(a.nwf + a.nwg + a.nwc + a.nw5 + a.nwx5 + a.nwx6 + a.npp, 256), 1024));
     }
     if (g.wbase) nwblk = 0;  // weight side prepared (cimq_module_prepare): the activation quantiser only
     if (fwd_actq_ok(g)) a.nact_blocks = 0;  // the forward's row staging quantises (stage_rows_q)
@@ -638,13 +666,16 @@ int cimq_module_route(const cimq_conv_desc* d, int* route) {
   if (g.input_kind != CIMQ_INPUT_RAW_LSQ) return fail(CIMQ_EINVAL, "module entry points take the raw activation");
   // the ctx / workspace layouts must not depend on state the entry points set only at launch (the
   // module path's NCHW flag): cimq_query_sizes, the prologue and the kernels compute them separately
+  // (the module path's ctx may END earlier -- no state-word region where its backward recomputes them -- and
+  // its backward's chunk / partial counts are that backward's; every offset and the workspace size agree)
   {
     Geo g1 = g;
     g1.onchw = 1;
     const CtxLayout a = ctx_layout(g), c = ctx_layout(g1);
     const WsLayout w0 = ws_layout(g), w1 = ws_layout(g1);
-    if (a.total != c.total || a.wbytes != c.wbytes || a.st != c.st || a.wg5 != c.wg5 || w0.total != w1.total ||
-        w0.nchunks_bwd != w1.nchunks_bwd || act_parts(g) != act_parts(g1))
+    if (c.total > a.total || a.wbytes != c.wbytes || a.st != c.st || a.wg5 != c.wg5 || a.wx6 != c.wx6 ||
+        w0.total != w1.total || w0.gw_slab != w1.gw_slab || w0.ga_slab != w1.ga_slab || w0.lsq_part != w1.lsq_part ||
+        (!r6_bwd(g1) && (w0.nchunks_bwd != w1.nchunks_bwd || act_parts(g) != act_parts(g1))))
       return fail(CIMQ_EINVAL, "internal: layouts depend on the output layout flag");
   }
   g.onchw = 1;  // the module path's layout (as module_forward_impl sets it)
@@ -657,7 +688,9 @@ int cimq_module_route(const cimq_conv_desc* d, int* route) {
   }
   // backward (dispatch_bwd_any)
   if (v7_bwd(g)) {
-    if (c1_plan(g).ok) {
+    if (r6_bwd(g)) {
+      route[1] = route[2] = CIMQ_ROUTE_R6;
+    } else if (c1_plan(g).ok) {
       route[1] = route[2] = CIMQ_ROUTE_C1;
     } else if (v9_plan(g).ok) {
       route[1] = route[2] = CIMQ_ROUTE_FUSED;

@@ -121,7 +121,9 @@ __device__ inline int f5_off(int NCB, int WP, int row, int cb, int col) { return
 #ifdef CIMQ_TU_FWD5  // defined in its launcher's translation unit only
 // NOB 16-channel output blocks per block (512 threads each): the NOB halves share the block's staged
 // activation patch (f5_plan: NOB = 2 where OB16 is even, one 1024-thread block per CU)
-template <int NOB>
+// WST: write the backward's state words and ctx (false where the module backward recomputes the partial sums,
+// cim_bwd_r6_kernel: the forward then writes only `out`, and its ADC epilogue skips the state-bit shifts)
+template <int NOB, bool WST>
 __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amdgpu_waves_per_eu(4, 4))) void cim_fwd5_kernel(
     Geo g, F5 v, const v4i* __restrict__ wf5, Params pp, const float* __restrict__ sw_p,
     const float* __restrict__ sa_p, const float* __restrict__ x, const float* __restrict__ sgn_p,
@@ -179,7 +181,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
   }
   act_lut_build_q<3>(g, sa, sgn, alut);  // entries 0 .. Qp + 1 (NaN), then the block barrier
   // ctx codes: the table grad_w expands them with (code e -> ctx word), written once per launch
-  if (v.codes && blockIdx.x == 0 && blockIdx.y == 0)
+  if (WST && v.codes && blockIdx.x == 0 && blockIdx.y == 0)
     for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x) cal[t] = alut[2 * t + 1];
 
   // this lane's A-operand pixel (image slot, output row / col) and its three position offsets
@@ -266,7 +268,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
           uint32_t P[4];
           tr4(w[0].x, w[1].x, w[2].x, w[3].x, P);
           dst[0] = P[0]; dst[4] = P[1]; dst[8] = P[2];
-          if (ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
+          if (WST && ih >= own_lo && ih < own_hi && cb0 + (qqs[u] >> 2) >= v.gown[q]) {
             if (v.codes) {  // one byte per element: grad_w expands it through the same word table
               uint8_t* cb8 = reinterpret_cast<uint8_t*>(xcb);
 #pragma unroll
@@ -332,9 +334,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
                 const int p = ps[k * 3 + j][r];
                 const uint64_t mhi = __builtin_amdgcn_ballot_w64(p >= pv.x);
                 const uint64_t mlo = __builtin_amdgcn_ballot_w64(p <= pv.y);
-                const uint64_t mps = __builtin_amdgcn_ballot_w64((unsigned)(p - pv.z) <= (unsigned)pv.w);
+                const uint64_t mps = WST ? __builtin_amdgcn_ballot_w64((unsigned)(p - pv.z) <= (unsigned)pv.w) : 0ull;
                 acc[r] += adc3(cf, mhi, mlo);
-                stw[r] = shin(shin(shin(stw[r], mlo), mhi | mlo), mps);
+                if (WST) stw[r] = shin(shin(shin(stw[r], mlo), mhi | mlo), mps);
               }
             }
           }
@@ -351,6 +353,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 acc[r] += adc_literal_sum(ps[k * 3 + j], g.mode, sw, sa, al, g.qn, g.qp, mk, r);
+                if (!WST) continue;
                 const bool pass = ste_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.thr_hi, g.thr_lo) != 0.f;
                 const float code = code_literal(ps[k * 3 + j][r], g.mode, sw, sa, al, g.qn, g.qp, g.thr_hi, g.thr_lo);
                 stw[r] |= st_bits(pass, code) << (3 * (k * 3 + j));
@@ -359,7 +362,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
           }
         }
         const int o = ob * 16 + r16;
-        if (o < g.O) {
+        if (WST && o < g.O) {
           const int s0 = (i * g.M + m0) * g.O + o;  // 32-bit: f5_plan bounds T * M * O
 #pragma unroll
           for (int r = 0; r < 4; ++r) st[s0 + r * g.O] = stw[r];

@@ -18,6 +18,7 @@
 #include "cimq_fwd5.hip"
 #include "cimq_gw5.hip"
 #include "cimq_gx5.hip"
+#include "cimq_r6.hip"
 
 
 namespace cimq {
@@ -157,7 +158,7 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
 inline bool dense_plan(const Geo& g);
 
 struct CtxLayout {
-  size_t xcode, xhat, alut, wfrag, wf5, wg5, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
+  size_t xcode, xhat, alut, wfrag, wf5, wg5, wx6, wgx, wcy, thi, tlo, mlo, mhi, coef, alpha, beta, bsum, ckj, flags, st;
   size_t lsq_scal;  // module entry points: sa, sw, alpha scale, max, min
   size_t wbytes;    // end of the weight-side regions
   size_t total;
@@ -165,6 +166,8 @@ struct CtxLayout {
 
 inline size_t f5_frag_bytes(const Geo& g);  // after f5_plan
 inline size_t x5_frag_bytes(const Geo& g);  // after x5_plan
+inline size_t r6_frag_bytes(const Geo& g);  // after r6_plan
+inline bool r6_bwd(const Geo& g);           // after r6_plan
 
 inline CtxLayout ctx_layout(const Geo& g) {
   CtxLayout L;
@@ -173,6 +176,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.wfrag = o; o = align256(o + (size_t)g.T * g.KS * g.NBLK * 64 * 16);
   L.wf5 = o; o = align256(o + f5_frag_bytes(g));  // cim_fwd5_kernel's weight operand
   L.wg5 = o; o = align256(o + x5_frag_bytes(g));  // cim_bwd_gx5_kernel's weight operand
+  L.wx6 = o; o = align256(o + r6_frag_bytes(g));  // cim_bwd_r6_kernel's gx operand
   L.wgx = o; o = align256(o + (size_t)g.T * g.FBT * g.NKS * 64 * 16);
   L.wcy = o; o = align256(o + (size_t)g.T * 12 * g.NKS * 64 * 16);  // v8 grad_x operand (<= 12 blocks / tile)
   L.thi = o; o = align256(o + npar * 4);
@@ -195,9 +199,12 @@ inline CtxLayout ctx_layout(const Geo& g) {
   // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three
   // 64-bit planes for w8a8) per (tile, pixel, channel)
   // (the dense path, cimq_part_dense.hip: a uint2 of three 16-bit planes per (i, m, o))
-  L.st = o; o = align256(o + std::max({(size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4),
-                                       (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24),
-                                       dense_plan(g) ? (size_t)g.T * g.M * g.O * 8 : (size_t)0}));
+  // (none where the module backward recomputes the partial sums, cim_bwd_r6_kernel: the region is last, so
+  // the module path's smaller ctx -- cimq_sizes.module_ctx_bytes -- keeps every other offset)
+  L.st = o; o = align256(o + (r6_bwd(g) ? (size_t)0
+                                        : std::max({(size_t)g.T * g.nbw * g.M * g.O * (g.NBP == 4 ? 2 : 4),
+                                                    (size_t)g.T * g.M * g.O * (g.NBP == 4 ? 4 : 24),
+                                                    dense_plan(g) ? (size_t)g.T * g.M * g.O * 8 : (size_t)0})));
   L.total = o;
   return L;
 }
@@ -876,6 +883,39 @@ inline size_t x5_frag_bytes(const Geo& g) {
   return p.ok ? (size_t)g.T * p.v.CBN * 9 * 2 * p.v.CBN * 64 * 16 : 0;
 }
 
+// ---- the whole backward of the w3a3 16 -> 16 stride-1 layers from recomputed partial sums (cimq_r6.hip) ----
+struct PlanR6 {
+  bool ok;
+  R6 v;
+  size_t lds;
+};
+
+inline PlanR6 r6_plan(const Geo& g) {
+  PlanR6 p;
+  memset(&p, 0, sizeof(p));
+  if (tune("R6", 1) == 0) return p;
+  // the module forward is cim_fwd5_kernel (its weight operand wf5 and activation word table are the recompute's),
+  // the library ternary ADC, w3a3 1-bit slices, 3x3 / stride 1 / pad 1, xbar 128, 16 -> 16 channels, 32 wide
+  const Plan5 p5 = f5_plan(g);
+  if (!p5.ok || !v7_bwd(g) || g.variant != VAR_LIBRARY || g.mode != ADC_TERNARY) return p;
+  if (g.input_kind != CIMQ_INPUT_RAW_LSQ || g.nbw != 3 || g.nba != 3 || g.bsw != 1 || g.bsa != 1) return p;
+  if (g.KH != 3 || g.KW != 3 || g.SH != 1 || g.SW != 1 || g.PH != 1 || g.PW != 1 || g.xbar != 128) return p;
+  if (g.C != kR6C || g.O != kR6C || g.W != kR6W || g.Wo != g.W || g.Ho != g.H || g.H % kR6R != 0) return p;
+  if (g.T != kR6T || g.lsq_qp >= 255.f || (long long)g.Nin >= (1LL << 31)) return p;
+  // one (tile, channel-block) pair per tile in the forward's operand
+  if (p5.v.ntc != kR6T || p5.v.tc0[0] != 0 || p5.v.tc0[1] != 1 || p5.v.tc0[2] != 2) return p;
+  for (int i = 0; i <= kR6T; ++i) p.v.tc0[i] = p5.v.tc0[i];
+  p.v.ntc = p5.v.ntc;
+  p.v.nmt = g.H / kR6R;
+  p.lds = R6L::LDS;
+  p.ok = true;
+  return p;
+}
+inline size_t r6_frag_bytes(const Geo& g) { return r6_plan(g).ok ? (size_t)kR6WxItems * 16 : 0; }
+// decided at launch: the module entry points (g.onchw) run cim_fwd5_kernel, whose operand the recompute needs; the
+// Function path's forward writes state words and keeps the state-word backward
+inline bool r6_bwd(const Geo& g) { return g.onchw && r6_plan(g).ok; }
+
 // The module path's ctx as ONE activation-code byte per element (instead of the 4-byte backward word):
 // where the forward is cim_fwd5_kernel (which quantises the activation itself) and the layer's grad_w
 // is cim_bwd_gw5_kernel (dispatch_bwd_any's order: c1, fused, then the v7 pair), the only ctx reader.
@@ -883,7 +923,7 @@ inline size_t x5_frag_bytes(const Geo& g) {
 // (c1_plan / v9_plan are declared above ws_layout.)
 inline bool ctx_codes(const Geo& g) {
   return g.onchw && fwd_actq_ok(g) && f5_plan(g).ok && v7_bwd(g) && !c1_plan(g).ok && !v9_plan(g).ok &&
-         g5_plan(g).ok;
+         g5_plan(g).ok && !r6_bwd(g);
 }
 
 struct WsLayout {
@@ -907,9 +947,10 @@ inline WsLayout ws_layout(const Geo& g) {
   const Plan7 p7 = v7_plan(g);
   const bool v7b = v7_bwd(g);
   const PlanG5 pg5 = g5_plan(g);
-  W.nchunks_bwd = (v9_plan(g).ok || c1_plan(g).ok) ? g.B : pg5.ok ? pg5.v.nchunks : v7b ? p7.v.nchunks
+  W.nchunks_bwd = (v9_plan(g).ok || c1_plan(g).ok || r6_bwd(g)) ? g.B : pg5.ok ? pg5.v.nchunks : v7b ? p7.v.nchunks
                 : dense_plan(g) ? cdiv(g.M, dense_rows_per_chunk(g)) : W.nchunks;
-  const size_t nch = (size_t)std::max(W.nchunks, W.nchunks_bwd);
+  // (sizes for either backward of a layer: the module path's recompute backward has one chunk per image)
+  const size_t nch = (size_t)std::max({W.nchunks, W.nchunks_bwd, r6_plan(g).ok ? g.B : 0});
   size_t o = 0;
   W.gw_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.FBT * 16 * g.Opad);
   W.ga_slab = o; o = align256(o + sizeof(float) * nch * g.T * g.nbw * g.nba * g.Opad);
@@ -1082,6 +1123,9 @@ int launch_fused(const Geo& g, const Plan9& p, const uint8_t* ctx, const float* 
                  const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq);
 int launch_c1(const Geo& g, const PlanC1& p, const uint8_t* ctx, const float* sw, const float* sa, const float* gout,
               const float* x, float* gx, uint8_t* ws, hipStream_t s, bool lsq);
+// cimq_part_r6.hip: the recompute backward (r6_bwd); dbg: the parity hook's state words into st_dbg instead
+int launch_r6(const Geo& g, const PlanR6& p, const uint8_t* ctx, const float* sw, const float* sa, const float* sgn,
+              const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s, uint32_t* st_dbg = nullptr);
 extern template CIMQ_V7_SIG(2, 2);
 extern template CIMQ_V7_SIG(3, 3);
 extern template CIMQ_V7_SIG(8, 8);

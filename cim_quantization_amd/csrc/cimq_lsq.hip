@@ -35,11 +35,12 @@ struct ModulePrep {
   v4i* wf5;   // cim_fwd5_kernel's weight operand (nw5 == 0 unless f5_plan applies)
   F5W f5;
   v4i* wg5;   // cim_bwd_gx5_kernel's weight operand (nwx5 == 0 unless x5_plan applies)
+  v4i* wx6;   // cim_bwd_r6_kernel's gx operand (nwx6 == 0 unless r6_plan applies)
   int ncpbt;
   Params pp;
   float* scal;  // [0] sa, [1] sw, [2] alpha scale, [3] max(alpha_cim), [4] min(alpha_cim)
   int nact_blocks;
-  int nwf, nwg, nwc, npp, nw5, nwx5;  // items of the weight-side roles
+  int nwf, nwg, nwc, npp, nw5, nwx5, nwx6;  // items of the weight-side roles
   const float* amm;             // wide alpha_cim: [namm][2] per-block (max, min) of alpha_minmax_kernel
   int namm;                     // 0: every weight block reduces alpha_cim itself
 };
@@ -135,14 +136,16 @@ __device__ inline void module_prep_weights(const Geo& g, const LsqArgs& q, const
       a.pp.flags[1] = a.pp.flags[2] = a.pp.flags[3] = 0;
     }
   }
-  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwc, e4 = e3 + a.nw5, e5 = e4 + a.nwx5, total = e5 + a.npp;
+  const int e1 = a.nwf, e2 = e1 + a.nwg, e3 = e2 + a.nwc, e4 = e3 + a.nw5, e5 = e4 + a.nwx5, e6 = e5 + a.nwx6,
+            total = e6 + a.npp;
   for (int t = wb * blockDim.x + threadIdx.x; t < total; t += nwblk * blockDim.x) {
     if (t < e1) wfrag_item(g, ws, a.wfrag, t);
     else if (t < e2) wgx_item(g, ws, a.wgx, t - e1);
     else if (t < e3) wcy_item(g, ws, a.ncpbt, a.wcy, t - e2);
     else if (t < e4) wf5_item(g, a.f5, ws, a.wf5, t - e3);
     else if (t < e5) wg5_item(g, ws, a.wg5, t - e4);
-    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e5, a.beta);
+    else if (t < e6) wx6_item(g, ws, a.wx6, t - e5);
+    else (void)params_item(g, as, sw, sa, a.bmask, a.pp, t - e6, a.beta);
   }
 }
 

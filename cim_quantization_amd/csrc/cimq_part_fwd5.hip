@@ -9,7 +9,10 @@ int launch_fwd5(const Geo& g, const Plan5& p, uint8_t* ctx, const float* sw, con
                 hipStream_t s, const ActQ* aq) {
   if (!p.ok || !aq || !g.onchw) return fail(CIMQ_EINVAL, "internal: cim_fwd5 off its plan");
   CtxLayout L = ctx_layout(g);
-  auto kern = p.nob == 2 ? cim_fwd5_kernel<2> : cim_fwd5_kernel<1>;
+  // the state words and ctx only where the backward reads them (not where cim_bwd_r6_kernel recomputes)
+  const bool wst = !r6_bwd(g);
+  auto kern = p.nob == 2 ? (wst ? cim_fwd5_kernel<2, true> : cim_fwd5_kernel<2, false>)
+                         : (wst ? cim_fwd5_kernel<1, true> : cim_fwd5_kernel<1, false>);
   CIMQ_TRY(set_lds(kern, p.lds));
   // 4 waves per SIMD: two 512-thread blocks per CU (one output block each) or one 1024-thread block (two),
   // a grid-stride walk over the 128-pixel m-tiles; the output-block groups in y

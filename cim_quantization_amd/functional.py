@@ -523,7 +523,8 @@ class _CimModuleConv(torch.autograd.Function):
         Ho = (H + 2 * pd[0] - KH) // st[0] + 1
         Wo = (W + 2 * pd[1] - KW) // st[1] + 1
         out = torch.empty(B, O, Ho, Wo, device=dev, dtype=torch.float32)
-        cbuf = torch.empty(max(sizes.ctx_bytes, 1), device=dev, dtype=torch.uint8)
+        # the module ctx: no per-partial-sum state words where the backward recomputes them (ABI 13)
+        cbuf = torch.empty(max(sizes.module_ctx_bytes, 1), device=dev, dtype=torch.uint8)
         ws = torch.empty(max(sizes.fwd_workspace_bytes, 1), device=dev, dtype=torch.uint8)
         lib = _lib.load()
         _lib.check(lib.cimq_module_forward(desc, lsq, xc.data_ptr(), wc.data_ptr(), aa.data_ptr(), aw.data_ptr(),
@@ -532,6 +533,7 @@ class _CimModuleConv(torch.autograd.Function):
                    "cimq_module_forward")
         ctx.desc, ctx.lsq, ctx.sizes = desc, lsq, sizes
         ctx.bufs = (xc, wc, aa, aw, ac, bm, sg, cbuf)
+        ctx.module_path = True  # a cimq_module_forward ctx (debug_state_codes)
         # the backward reads x and the raw parameters again (act-LSQ / weight-LSQ STE); saving
         # them lets autograd's version counters catch an in-place change in between
         ctx.save_for_backward(x, weight, alpha_act, alpha_weight, alpha_cim)
@@ -807,6 +809,15 @@ def debug_state_codes(out):
     shape = (d.batch, T, nbw, nba, Ho * Wo, d.out_channels)
     code = torch.empty(shape, device=cbuf.device, dtype=torch.int8)
     passed = torch.empty(shape, device=cbuf.device, dtype=torch.uint8)
+    if getattr(ctx, "module_path", False) and _lib.module_route(d)[1] == _lib.CIMQ_ROUTE_R6:
+        # a module layer whose backward recomputes the partial sums: its forward left no state words, so the
+        # codes come from the recomputing backward's own code path (cimq_debug_recompute_codes)
+        xc, sg = ctx.bufs[0], ctx.bufs[6]
+        st = torch.empty(T * d.batch * Ho * Wo * d.out_channels * 4, device=cbuf.device, dtype=torch.uint8)
+        _lib.check(_lib.load().cimq_debug_recompute_codes(d, xc.data_ptr(), sg.data_ptr(), cbuf.data_ptr(),
+                                                          st.data_ptr(), code.data_ptr(), passed.data_ptr(),
+                                                          _stream()), "cimq_debug_recompute_codes")
+        return code, passed
     _lib.check(_lib.load().cimq_debug_state_codes(d, cbuf.data_ptr(), code.data_ptr(), passed.data_ptr(), _stream()),
                "cimq_debug_state_codes")
     return code, passed

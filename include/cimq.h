@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 12
+#define CIMQ_ABI_VERSION 13
 
 /* status codes */
 #define CIMQ_OK 0
@@ -113,6 +113,9 @@ typedef struct cimq_sizes {
   size_t fwd_workspace_bytes; /* scratch for cimq_forward / cimq_alpha_init */
   size_t bwd_workspace_bytes; /* scratch for cimq_backward */
   size_t wprep_bytes;         /* weight-side state of the module entry points (cimq_module_prepare) */
+  size_t module_ctx_bytes;    /* ctx of the module entry points (cimq_module_forward / _backward): smaller than
+                                 ctx_bytes where their backward recomputes the partial sums instead of reading
+                                 per-partial-sum state words (CIMQ_ROUTE_R6).  Since ABI 13 */
 } cimq_sizes;
 
 /* ABI version of the loaded library (compare with CIMQ_ABI_VERSION). */
@@ -152,8 +155,8 @@ int cimq_backward(const cimq_conv_desc* d, const float* grad_out, const float* x
  * the activation, weight and alpha_cim quantisers run inside the library on the raw
  * parameters, then the CiM conv; ``out`` is the module's NCHW output [B, O, Ho, Wo] (before
  * the optional bias).  Requires input_kind = CIMQ_INPUT_RAW_LSQ.  ``alpha_cim`` may be NULL
- * unless adc_bits is 1 or 1.5.  ``ctx`` must hold cimq_query_sizes()->ctx_bytes and ``ws``
- * fwd_workspace_bytes. */
+ * unless adc_bits is 1 or 1.5.  ``ctx`` must hold cimq_query_sizes()->module_ctx_bytes (ABI 13; ctx_bytes
+ * is never smaller) and ``ws`` fwd_workspace_bytes. */
 int cimq_module_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
                         const float* alpha_act, const float* alpha_weight, const float* alpha_cim,
                         const int8_t* binary_mask, const float* signed_act, float* out, void* ctx, void* ws,
@@ -214,7 +217,9 @@ enum {
   CIMQ_ROUTE_C1 = 5,       /* the w8a8 first conv: cim_bwd_c1_kernel (both) */
   CIMQ_ROUTE_GX5 = 6,      /* grad_x: cim_bwd_gx5_kernel (per input pixel, round 5) */
   CIMQ_ROUTE_GW5 = 7,      /* grad_w: cim_bwd_gw5_kernel (A-ready patch, round 5) */
-  CIMQ_ROUTE_DENSE = 8     /* the dense 1x1 path */
+  CIMQ_ROUTE_DENSE = 8,    /* the dense 1x1 path */
+  CIMQ_ROUTE_R6 = 9        /* grad_x and grad_w in cim_bwd_r6_kernel from RECOMPUTED partial sums (the forward
+                              writes no state words; round 6, ABI 13) */
 };
 int cimq_module_route(const cimq_conv_desc* d, int* route);
 int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,
@@ -323,6 +328,14 @@ int cimq_debug_partial_sums(const cimq_conv_desc* d, const float* x, const float
  * CIMQ_EUNSUPPORTED for layers whose forward writes no state words. */
 int cimq_debug_state_codes(const cimq_conv_desc* d, const void* ctx, int8_t* code_out, uint8_t* pass_out,
                            void* stream);
+
+/* Parity hook for the module layers whose backward recomputes the partial sums (CIMQ_ROUTE_R6, whose forward
+ * leaves no state words): the ADC codes and STE pass bits as cimq_debug_state_codes gives them, produced by the
+ * recomputing backward's own code path (cim_bwd_r6_kernel in its debug form) from x, signed_act and the ctx of
+ * cimq_module_forward.  ``st_scratch`` is caller-owned device memory of T * B * Ho * Wo * O * 4 bytes.
+ * CIMQ_EUNSUPPORTED for other layers.  Since ABI 13. */
+int cimq_debug_recompute_codes(const cimq_conv_desc* d, const float* x, const float* signed_act, const void* ctx,
+                               void* st_scratch, int8_t* code_out, uint8_t* pass_out, void* stream);
 
 /* ---- plain LSQ modules (lsq.py:389-436 Conv2dLSQ, :591-617 LinearLSQ, :620-662 ActLSQ) ---- */
 
