@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CIMQ_LIB_PATH") or os.path.join(_HERE, "libcimq.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 CIMQ_EINVAL = 1  # include/cimq.h error codes
 CIMQ_EUNSUPPORTED = 2
@@ -33,6 +33,7 @@ CIMQ_ADC_SHIFT_ROUND = 2
 CIMQ_ADC_SHIFT_SIGN = 3
 CIMQ_ADC_F_PS_INT8 = 0x100
 CIMQ_ADC_F_SHIFT_RANGE = 0x200
+CIMQ_OPT_RECOMPUTE = 1  # cimq_conv_desc.options (ABI 14)
 
 # every symbol include/cimq.h declares
 EXPORTED_SYMBOLS = (
@@ -96,7 +97,7 @@ class ConvDesc(ctypes.Structure):
         ("lsq_qp", ctypes.c_float),
         ("adc_variant", ctypes.c_int32),
         ("seed_lo", ctypes.c_uint32), ("seed_hi", ctypes.c_uint32),
-        ("reserved", ctypes.c_int32),
+        ("options", ctypes.c_int32),
     ]
 
 
@@ -257,7 +258,7 @@ def check(rc: int, what: str):
 
 
 def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w, bs_a, adc_bits,
-              input_kind=CIMQ_INPUT_XQ, lsq_qp=0.0, adc_variant=CIMQ_ADC_LIBRARY, seed=0) -> ConvDesc:
+              input_kind=CIMQ_INPUT_XQ, lsq_qp=0.0, adc_variant=CIMQ_ADC_LIBRARY, seed=0, options=0) -> ConvDesc:
     d = ConvDesc()
     d.batch, d.in_channels, d.in_h, d.in_w = int(B), int(C), int(H), int(W)
     d.out_channels, d.kernel_h, d.kernel_w = int(O), int(KH), int(KW)
@@ -270,6 +271,7 @@ def make_desc(B, C, H, W, O, KH, KW, stride, padding, xbar, bits_w, bits_a, bs_w
     d.lsq_qp = float(lsq_qp)
     d.adc_variant = int(adc_variant)
     d.seed_lo, d.seed_hi = int(seed) & 0xFFFFFFFF, (int(seed) >> 32) & 0xFFFFFFFF
+    d.options = int(options)
     return d
 
 

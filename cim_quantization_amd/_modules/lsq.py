@@ -69,6 +69,10 @@ class Conv2dLSQCiM(_Conv2dQCiM):
         # AccumulateGrad kernels); set by dist.GradBucket.own(), which owns the exchange
         self.accumulate_grads_in_place = False
         self.tail_stream = None  # GradBucket.own(overlap=True): stream of the parameter-gradient epilogue
+        # CIMQ_OPT_RECOMPUTE: where the library has a recompute backward for this shape, keep no per-partial-sum
+        # state words between forward and backward (33.5 MB less per 16-channel ResNet-20 layer at B = 256) and
+        # recompute the partial sums in the backward -- slower on MI355X, so off by default
+        self.recompute_psum = False
         self._wprep = None        # functional.prepare_weights: the next forward's weight side, computed ahead
         self._last_x_shape = None
 
@@ -133,7 +137,8 @@ class Conv2dLSQCiM(_Conv2dQCiM):
                                   self.nbits_a, self.abitslice, self.nbits_w, self.wbitslice, self.adcbits,
                                   self.xbar, self.nbits_alpha, self.accumulate_grads_in_place,
                                   bool(self.stochastic_quant),
-                                  self.tail_stream if self.accumulate_grads_in_place else None, wprep)
+                                  self.tail_stream if self.accumulate_grads_in_place else None, wprep,
+                                  self.recompute_psum)
             if self.bias is not None:
                 out = out + self.bias  # broadcasts over the last axis, as lsq.py:583
             return out

@@ -867,9 +867,9 @@ int cimq_module_backward_params(const cimq_conv_desc* d, const cimq_lsq_desc* q,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint8_t* c = reinterpret_cast<const uint8_t*>(ctx);
   uint8_t* w = reinterpret_cast<uint8_t*>(ws);
+  if (v3_plan(g).ok) g.onchw = 1;  // as module_backward_impl: the backward that ran was the module path's
   if (gw_deferrable(g)) {
     // the grad_w kernel cimq_module_backward left out (grad_out NCHW, as the v7 path reads it there)
-    g.onchw = 1;
     const float* scal = reinterpret_cast<const float*>(wreg(g, c) + ctx_layout(g).lsq_scal);
     bool lsq_fused = false;
     CIMQ_TRY(dispatch_bwd_any(g, c, scal + 1, scal, nullptr, grad_out, nullptr, nullptr, w, s, &lsq_fused, 2));

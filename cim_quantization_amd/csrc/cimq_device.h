@@ -41,6 +41,7 @@ struct Geo {
   int onchw;               // out / grad_out layout: 0 = [B, P, O] (the Function's), 1 = NCHW (the module's)
   int variant;             // AdcVariant; anything but VAR_LIBRARY runs the literal (general) kernels
   int ps_int8;             // partial sums pass an int8 buffer before the ADC (scale_shift.py:401)
+  int recompute;           // cimq_conv_desc.options & CIMQ_OPT_RECOMPUTE: the module backward recomputes partial sums
   uint32_t seed_lo, seed_hi;  // VAR_STOCHASTIC: Philox key
   const unsigned char* wbase;  // host side: the weight-side ctx regions (cimq_lsq_desc.wprep); null: inside ctx
 };

@@ -124,6 +124,8 @@ inline int make_geo(const cimq_conv_desc* d, Geo* out) {
   g.ps_int8 = (d->adc_variant & CIMQ_ADC_F_PS_INT8) ? 1 : 0;
   g.seed_lo = d->seed_lo;
   g.seed_hi = d->seed_hi;
+  if (d->options & ~CIMQ_OPT_RECOMPUTE) return fail(CIMQ_EINVAL, "unknown options 0x%x", d->options);
+  g.recompute = (d->options & CIMQ_OPT_RECOMPUTE) ? 1 : 0;
   switch (g.variant) {
     case VAR_LIBRARY: break;
     case VAR_STOCHASTIC:  // lsq.py:136-137: the stochastic ADC is the 1.5-bit one
@@ -893,7 +895,7 @@ struct PlanR6 {
 inline PlanR6 r6_plan(const Geo& g) {
   PlanR6 p;
   memset(&p, 0, sizeof(p));
-  if (tune("R6", 1) == 0) return p;
+  if (!g.recompute || tune("R6", 1) == 0) return p;  // the caller's choice (CIMQ_OPT_RECOMPUTE)
   // the module forward is cim_fwd5_kernel (its weight operand wf5 and activation word table are the recompute's),
   // the library ternary ADC, w3a3 1-bit slices, 3x3 / stride 1 / pad 1, xbar 128, 16 -> 16 channels, 32 wide
   const Plan5 p5 = f5_plan(g);

@@ -243,6 +243,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   };
 
   const int nmt = v.nmt;
+#ifdef CIMQ_EXP_R6_WFPF
+  v4i wnx[9];  // the next tile's forward weight fragments, in flight one tile ahead
+#pragma unroll
+  for (int q = 0; q < 9; ++q) wnx[q] = wf5[(size_t)v.tc0[0] * 9 * 64 + lane + q * 64];
+#endif
   float xv[2][4];
   stage_load(0, xv);
   float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -266,10 +271,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
 #pragma unroll 1
     for (int i = 0; i < T; ++i) {
       // the tile's forward weight fragments [s][k] (cim_fwd5_kernel's operand, output block 0)
-      const v4i* wt = wf5 + (size_t)v.tc0[i] * 9 * 64 + lane;
       v4i wfr[9];
+#ifdef CIMQ_EXP_R6_WFPF
+      {
+        const v4i* wt = wf5 + (size_t)v.tc0[i + 1 < T ? i + 1 : 0] * 9 * 64 + lane;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          wfr[q] = wnx[q];
+          wnx[q] = wt[q * 64];
+        }
+      }
+#else
+      const v4i* wt = wf5 + (size_t)v.tc0[i] * 9 * 64 + lane;
 #pragma unroll
       for (int q = 0; q < 9; ++q) wfr[q] = wt[q * 64];
+#endif
       v4i ps[9];
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
@@ -398,6 +414,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     }
     __syncthreads();  // (B1) the G patch is complete; the patches' readers are done
     if (more) stage_store(r0 + R, xv);  // the next m-tile's patches (its phase A reads them after B4)
+#ifdef CIMQ_EXP_R6_XFPF
+    float4 xf[2];  // the finished rows' x (act-LSQ backward), in flight behind the gx MFMAs
+    {
+      const int t = (int)threadIdx.x;
+      const int cc = t & 127, part = t >> 7;
+      const int c = cc >> 3, iw = 4 * (cc & 7);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int ih = part == 0 ? r0 - 1 + u : r0 + part;  // part 0: rows r0 - 1, r0; part p: row r0 + p
+        xf[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((u == 0 || part == 0) && (unsigned)ih < (unsigned)H)
+          xf[u] = *reinterpret_cast<const float4*>(x + ((b * C + c) * H + ih) * W + iw);
+      }
+    }
+#endif
     if (DBG) {
       __syncthreads();
       gq = gqn;
@@ -444,9 +475,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
         return *reinterpret_cast<const float4*>(smem + O_GP + (kh * R + rs) * GROW + GPX + (c * EXP + iw) * 4);
       };
       float4* ca = reinterpret_cast<float4*>(smem + O_CA);
-      auto fin = [&](int ih, float4 v4) {
+      auto fin = [&](int ih, float4 v4, int u) {
         const int gi = ((b * C + c) * H + ih) * W + iw;
+#ifdef CIMQ_EXP_R6_XFPF
+        const float4 xv4 = xf[u];
+#else
+        (void)u;
         const float4 xv4 = *reinterpret_cast<const float4*>(x + gi);
+#endif
         const float xs[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
         const float vs[4] = {v4.x, v4.y, v4.z, v4.w};
         float o4[4];
@@ -469,18 +505,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
       auto add4 = [](float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); };
       if (part == 0) {
         const int ci = c * W + iw;
-        if (n > 0) fin(r0 - 1, add4(exr(0, 0), ca[ci >> 2]));
+        if (n > 0) fin(r0 - 1, add4(exr(0, 0), ca[ci >> 2]), 0);
         float4 v0 = add4(exr(0, 1), exr(1, 0));
         if (n > 0) v0 = add4(v0, ca[(C * W + ci) >> 2]);
-        fin(r0, v0);
+        fin(r0, v0, 1);
         if (more) {
           ca[ci >> 2] = add4(exr(1, R - 1), exr(2, R - 2));  // input row r0 + R - 1: kh 1 and 2
           ca[(C * W + ci) >> 2] = exr(2, R - 1);             // input row r0 + R: kh 2
         }
       } else if (part < R - 1) {
-        fin(r0 + part, add4(add4(exr(0, part + 1), exr(1, part)), exr(2, part - 1)));
+        fin(r0 + part, add4(add4(exr(0, part + 1), exr(1, part)), exr(2, part - 1)), 0);
       } else if (!more) {
-        fin(r0 + R - 1, add4(exr(1, R - 1), exr(2, R - 2)));
+        fin(r0 + R - 1, add4(exr(1, R - 1), exr(2, R - 2)), 0);
       }
     }
     __syncthreads();  // (B4) the exchange is read: the next m-tile's G writes may begin

@@ -54,9 +54,12 @@ class GradBucket:
             self.views.append(self.flat[off:off + p.numel()].view_as(p))
             off += p.numel()
         self.nbytes = n * 4
+        self.bounds = [0]  # parameter boundaries in the bucket: segments start and end on them
+        for p in self.params:
+            self.bounds.append(self.bounds[-1] + p.numel())
         self.reattached = 0  # gradients found detached from the bucket (diagnostic)
         self.side = None  # stream of the overlapped parameter-gradient epilogues (own(overlap=True))
-        self._works, self._sent = [], 0  # segments already in flight (exchange_segment)
+        self._works, self._ranges, self._sent = [], [], 0  # segments in flight; end of the forward run
         self._attach()
 
     def _attach(self):
@@ -89,10 +92,18 @@ class GradBucket:
         if self.side is not None:
             torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
 
-    def sync_views(self):
-        """Make every ``p.grad`` the bucket view again, copying gradients that autograd put in
-        fresh tensors (after ``zero_grad(set_to_none=True)`` or a reassigned ``.grad``)."""
-        for p, v in zip(self.params, self.views):
+    def _in(self, i, ranges):
+        lo, hi = self.bounds[i], self.bounds[i + 1]
+        return any(a <= lo and hi <= b for a, b in ranges)
+
+    def sync_views(self, lo=0, hi=None):
+        """Make every ``p.grad`` whose slot lies in ``flat[lo:hi]`` the bucket view again, copying
+        gradients that autograd put in fresh tensors (after ``zero_grad(set_to_none=True)`` or a
+        reassigned ``.grad``).  Never touches a slot whose segment is still being reduced."""
+        hi = self.flat.numel() if hi is None else hi
+        for i, (p, v) in enumerate(zip(self.params, self.views)):
+            if not (lo <= self.bounds[i] and self.bounds[i + 1] <= hi) or self._in(i, self._ranges):
+                continue
             g = p.grad
             if g is not None and g.data_ptr() == v.data_ptr() and g.shape == v.shape:
                 continue
@@ -103,39 +114,80 @@ class GradBucket:
                 v.copy_(g.detach().reshape(v.shape))
             p.grad = v
 
-    def exchange_segment(self, hi, group=None):
-        """Start summing ``flat[sent:hi]`` over the ranks of ``group`` without waiting for it: the
-        gradients of the layers whose backward (and epilogue) has finished, while the backward of
-        the next layers runs.  Segments go out in bucket order, each from where the last one ended;
-        ``exchange()`` sends the rest, waits for all of them and averages.  On RCCL the collective
+    def span(self, params):
+        """``(lo, hi)``: the bucket range holding the gradients of ``params`` (contiguous in the
+        bucket, e.g. one layer's parameters), for ``exchange_range``."""
+        ids = {id(p) for p in params}
+        idx = [i for i, p in enumerate(self.params) if id(p) in ids]
+        if not idx or idx != list(range(idx[0], idx[-1] + 1)):
+            raise ValueError("span: the parameters are not one contiguous run of the bucket")
+        return self.bounds[idx[0]], self.bounds[idx[-1] + 1]
+
+    def exchange_range(self, lo, hi, group=None):
+        """Start summing ``flat[lo:hi]`` over the ranks of ``group`` without waiting for it: the
+        gradients of layers whose backward (and epilogue) has FINISHED, while the backward of the
+        other layers runs.  Ranges may go out in any order -- bucket order (``exchange_segment``),
+        or reverse order as a network's backward finishes its last layers first -- but must start
+        and end on parameter boundaries and must not overlap a range already in flight (ValueError).
+        The caller guarantees completion: every gradient in the range is written (on the current
+        stream, or on the bucket's side stream, which is joined first) and nothing writes it again
+        before ``exchange()``; the bucket itself never touches a range in flight.  ``exchange()``
+        sends what no range covered, waits for every range and averages.  On RCCL the collective
         runs on the process group's stream, ordered after the work already on the current stream,
-        so the next segment's kernels overlap it.  Each element is reduced by one collective whatever
-        the segmentation: with two ranks the sum is bit-identical to the single-bucket exchange
-        (fp32 addition commutes); with more, the ring's order of additions can differ in the last
-        bit.  No-op for a single process."""
+        so later kernels overlap it.  Each element is reduced by one collective whatever the
+        segmentation: with two ranks the sum is bit-identical to the single-bucket exchange (fp32
+        addition commutes); with more, the ring's order of additions can differ in the last bit.
+        No-op for a single process."""
+        if _world(group) <= 1 or hi <= lo:
+            return
+        if lo not in self.bounds or hi not in self.bounds:
+            raise ValueError(f"exchange_range({lo}, {hi}): not on parameter boundaries")
+        if any(lo < b and a < hi for a, b in self._ranges):
+            raise ValueError(f"exchange_range({lo}, {hi}) overlaps a range already in flight")
+        self.join()
+        self.sync_views(lo, hi)
+        self._works.append(dist.all_reduce(self.flat[lo:hi], group=group, async_op=True))
+        self._ranges.append((lo, hi))
+
+    def exchange_segment(self, hi, group=None):
+        """``exchange_range`` from where the last bucket-order segment ended (0 first) to ``hi``:
+        for backward passes that finish layers in parameter order (bench.Trainer runs each layer's
+        fwd+bwd in turn).  A segment already sent is a no-op."""
         if _world(group) <= 1 or hi <= self._sent:
             return
-        self.join()
-        self.sync_views()
-        self._works.append(dist.all_reduce(self.flat[self._sent:hi], group=group, async_op=True))
+        self.exchange_range(self._sent, hi, group)
         self._sent = hi
 
+    def _wait_pending(self):
+        for w in self._works:
+            w.wait()
+        had = bool(self._works)
+        self._works, self._ranges, self._sent = [], [], 0
+        return had
+
     def exchange(self, group=None):
-        """Average the bucket over the ranks of ``group`` (no-op for a single process): the part no
-        ``exchange_segment`` sent, then the wait for every segment, then one scale."""
+        """Average the bucket over the ranks of ``group`` (no-op for a single process): the parts no
+        ``exchange_range`` sent, then the wait for every range, then one scale.  A gradient found
+        detached from a slot that already went out raises: the range sent a stale value."""
         self.join()
-        self.sync_views()
+        for i, (p, v) in enumerate(zip(self.params, self.views)):
+            if self._in(i, self._ranges) and p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                self._wait_pending()
+                raise RuntimeError("exchange: a gradient was detached from a bucket range already sent")
+        self.sync_views()  # the slots outside the ranges in flight
         world = _world(group)
         if world > 1:
-            if self._sent < self.flat.numel():
-                dist.all_reduce(self.flat[self._sent:], group=group)
-            for w in self._works:
-                w.wait()
-            self._works, self._sent = [], 0
+            lo = 0
+            for a, b in sorted(self._ranges) + [(self.flat.numel(), self.flat.numel())]:
+                if a > lo:
+                    dist.all_reduce(self.flat[lo:a], group=group)
+                lo = max(lo, b)
+            self._wait_pending()
             self.flat.mul_(1.0 / world)
 
     def zero(self):
         self.join()
+        self._wait_pending()  # a reduction still in flight would write after the zeroing
         self.flat.zero_()
         self._attach()
 
@@ -145,6 +197,7 @@ class GradBucket:
         data-dependent step sizes (module docstring).  One coalesced collective per dtype."""
         if _world(group) <= 1:
             return
+        self._wait_pending()
         seen, tensors = set(), []
         for t in list(self.params) + [b for m in modules for b in m.buffers()]:
             if id(t) not in seen:
@@ -212,6 +265,8 @@ class FlatSGD:
         the update is one libcimq launch (cimq_flat_sgd; torch's elementwise ops took four);
         ``zero_grad`` also zeroes the bucket's gradients in it."""
         self.bucket.join()
+        if self.bucket._wait_pending():
+            raise RuntimeError("FlatSGD.step: exchange segments in flight; call bucket.exchange() first")
         self.bucket.sync_views()
         if self.flat.is_cuda:
             from . import _lib

@@ -419,7 +419,7 @@ def _versions(*ts):
 
 
 def _module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits,
-                  xbar, nbits_alpha, has_alpha, stochastic):
+                  xbar, nbits_alpha, has_alpha, stochastic, recompute=False):
     B, C, H, W = x_shape
     O, _, KH, KW = weight.shape
     st = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
@@ -429,7 +429,8 @@ def _module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice
     desc = _lib.make_desc(B, C, H, W, O, KH, KW, st, pd, xbar, nbits_w, nbits_a, wbitslice,
                           abitslice, adcbits, _lib.CIMQ_INPUT_RAW_LSQ, qp_a,
                           _lib.CIMQ_ADC_STOCHASTIC if stochastic else _lib.CIMQ_ADC_LIBRARY,
-                          stochastic_seed() if stochastic else 0)
+                          stochastic_seed() if stochastic else 0,
+                          _lib.CIMQ_OPT_RECOMPUTE if recompute else 0)
     lsq = _lib.make_lsq_desc(qn_w, qp_w, 1.0 / math.sqrt(B * C * H * W * qp_a),
                              1.0 / math.sqrt(weight.numel() * qp_w), nbits_alpha if has_alpha else 0)
     return desc, lsq
@@ -451,7 +452,8 @@ def prepare_weights(modules, stream=None):
         shape = m._last_x_shape
         has_alpha = m.alpha_cim is not None
         desc, lsq = _module_descs(shape, m.weight, m.stride, m.padding, m.dilation, m.nbits_a, m.abitslice,
-                                  m.nbits_w, m.wbitslice, m.adcbits, m.xbar, m.nbits_alpha, has_alpha, False)
+                                  m.nbits_w, m.wbitslice, m.adcbits, m.xbar, m.nbits_alpha, has_alpha, False,
+                                  bool(getattr(m, "recompute_psum", False)))
         sizes = _lib.query_sizes(desc)
         dev = m.weight.device
         buf = torch.empty(max(sizes.wprep_bytes, 1), device=dev, dtype=torch.uint8)
@@ -500,12 +502,12 @@ class _CimModuleConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                 dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha, accumulate=False,
-                stochastic=False, tail_stream=None, wprep=None):
+                stochastic=False, tail_stream=None, wprep=None, recompute=False):
         _require_device(x)
         dev = x.device
         B, C, H, W, O, KH, KW, st, pd = _geometry(x, weight, stride, padding, dilation)
         desc, lsq = _module_descs(tuple(x.shape), weight, st, pd, dilation, nbits_a, abitslice, nbits_w, wbitslice,
-                                  adcbits, xbar, nbits_alpha, alpha_cim is not None, stochastic)
+                                  adcbits, xbar, nbits_alpha, alpha_cim is not None, stochastic, recompute)
         # a prepared weight side (prepare_weights) if it was made for exactly this call
         ctx.wprep_buf = None
         if (wprep is not None and not stochastic and wprep.key == _prep_key(desc, lsq, x.shape)
@@ -599,7 +601,7 @@ class _CimModuleConv(torch.autograd.Function):
                                                       None if gac is None else gac.data_ptr(), ws.data_ptr(),
                                                       ch.pending, stream), "cimq_module_backward_chain")
             ch.add((ws, cbuf, wc, ac, gw, gaa, gaw, gac, ctx.wprep_buf))
-            return (gx,) + (None,) * 20
+            return (gx,) + (None,) * 21
         _lib.check(lib.cimq_module_backward(ctx.desc, lsq, g.data_ptr(), xc.data_ptr(), wc.data_ptr(),
                                             aa.data_ptr(), aw.data_ptr(), None if ac is None else ac.data_ptr(),
                                             bm.data_ptr(), sg.data_ptr(), cbuf.data_ptr(), gx.data_ptr(),
@@ -621,20 +623,21 @@ class _CimModuleConv(torch.autograd.Function):
                     ((ctx.wprep_buf,) if ctx.wprep_buf is not None else ()):
                 t.record_stream(side)
         if targets is not None:
-            return (gx,) + (None,) * 20
-        return (gx, gw, gaa, gaw, gac) + (None,) * 16
+            return (gx,) + (None,) * 21
+        return (gx, gw, gaa, gaw, gac) + (None,) * 17
 
 
 def cim_module_conv(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride, padding,
                     dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar, nbits_alpha,
-                    accumulate=False, stochastic=False, tail_stream=None, wprep=None):
+                    accumulate=False, stochastic=False, tail_stream=None, wprep=None, recompute=False):
     """NCHW output of a Conv2dLSQCiM layer (quantisers fused); differentiable in x, weight and
     the three step-size parameters (alpha_act and alpha_weight are 1-element tensors).
     ``accumulate`` / ``tail_stream``: see _CimModuleConv; ``stochastic``: the stochastic 1.5-bit ADC;
-    ``wprep``: a WeightPrep from prepare_weights (used only if it matches this call)."""
+    ``wprep``: a WeightPrep from prepare_weights (used only if it matches this call); ``recompute``:
+    CIMQ_OPT_RECOMPUTE (no state words in the ctx where a recompute backward exists; slower)."""
     return _CimModuleConv.apply(x, weight, alpha_act, alpha_weight, alpha_cim, binary_mask, signed_act, stride,
                                 padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, adcbits, xbar,
-                                nbits_alpha, accumulate, stochastic, tail_stream, wprep)
+                                nbits_alpha, accumulate, stochastic, tail_stream, wprep, recompute)
 
 
 def _shift_module_descs(x_shape, weight, stride, padding, dilation, nbits_a, abitslice, nbits_w, wbitslice, xbar,

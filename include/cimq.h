@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CIMQ_ABI_VERSION 13
+#define CIMQ_ABI_VERSION 14
 
 /* status codes */
 #define CIMQ_OK 0
@@ -66,6 +66,13 @@ extern "C" {
                                         but 1 (scale_shift.py:369-375) instead of the library's
                                         +-1 for 1.5 bits */
 
+/* cimq_conv_desc.options */
+#define CIMQ_OPT_RECOMPUTE 1 /* module entry points: where a recompute backward exists (CIMQ_ROUTE_R6: w3a3 16 -> 16,
+                                3x3 stride 1, xbar 128, 32 wide) the forward writes no per-partial-sum state words
+                                and the backward recomputes the partial sums -- a smaller ctx (module_ctx_bytes;
+                                33.5 MB less per such layer at B = 256) for a slower backward on MI355X (DESIGN.md
+                                section 10).  Ignored elsewhere.  Since ABI 14 */
+
 /* cimq_lsq_desc.flags */
 #define CIMQ_LSQ_ACCUMULATE_GRADS 1 /* cimq_module_backward adds the parameter gradients into
                                        grad_weight / grad_alpha_* (torch's AccumulateGrad,
@@ -91,7 +98,7 @@ typedef struct cimq_conv_desc {
   float lsq_qp;       /* CIMQ_INPUT_RAW_LSQ: act clamp max Qp_a = 2^bits_a - 1 (Qn_a = 0) */
   int32_t adc_variant; /* CIMQ_ADC_* | CIMQ_ADC_F_* (0: the library ADC) */
   uint32_t seed_lo, seed_hi; /* CIMQ_ADC_STOCHASTIC: Philox key of this call */
-  int32_t reserved;
+  int32_t options;    /* CIMQ_OPT_* bits (0: the defaults); was ``reserved`` before ABI 14 */
 } cimq_conv_desc;
 
 /* The LSQ quantisers of Conv2dLSQCiM.forward (lsq.py:544-571), for the module entry points. */
@@ -115,7 +122,7 @@ typedef struct cimq_sizes {
   size_t wprep_bytes;         /* weight-side state of the module entry points (cimq_module_prepare) */
   size_t module_ctx_bytes;    /* ctx of the module entry points (cimq_module_forward / _backward): smaller than
                                  ctx_bytes where their backward recomputes the partial sums instead of reading
-                                 per-partial-sum state words (CIMQ_ROUTE_R6).  Since ABI 13 */
+                                 per-partial-sum state words (CIMQ_ROUTE_R6 under CIMQ_OPT_RECOMPUTE).  Since ABI 13 */
 } cimq_sizes;
 
 /* ABI version of the loaded library (compare with CIMQ_ABI_VERSION). */
@@ -219,7 +226,7 @@ enum {
   CIMQ_ROUTE_GW5 = 7,      /* grad_w: cim_bwd_gw5_kernel (A-ready patch, round 5) */
   CIMQ_ROUTE_DENSE = 8,    /* the dense 1x1 path */
   CIMQ_ROUTE_R6 = 9        /* grad_x and grad_w in cim_bwd_r6_kernel from RECOMPUTED partial sums (the forward
-                              writes no state words; round 6, ABI 13) */
+                              writes no state words; round 6, ABI 13; only under CIMQ_OPT_RECOMPUTE since ABI 14) */
 };
 int cimq_module_route(const cimq_conv_desc* d, int* route);
 int cimq_module_shift_forward(const cimq_conv_desc* d, const cimq_lsq_desc* q, const float* x, const float* weight,

@@ -173,51 +173,56 @@ def test_pending_host_logic(lib):
 
 
 def test_module_route_resnet20(lib):
-    """cimq_module_route (ABI 12; CIMQ_ROUTE_R6 since ABI 13): which kernels the module entry points run for each
-    ResNet-20 layer of the benchmark (bench.RESNET20, xbar 128, adc 1.5, B = 256) -- the round-6 recompute
-    backward on the 16-channel stride-1 layers, the round-5 kernels where their plans apply,
-    the round-4 ones elsewhere.  A host query: no device work."""
+    """cimq_module_route (ABI 12; CIMQ_ROUTE_R6 since ABI 13, under CIMQ_OPT_RECOMPUTE since ABI 14): which kernels
+    the module entry points run for each ResNet-20 layer of the benchmark (bench.RESNET20, xbar 128, adc 1.5,
+    B = 256) -- the round-5 kernels where their plans apply, the round-4 ones elsewhere, and
+    with the recompute option the round-6 recompute backward on the 16-channel stride-1 layers.  A host query: no
+    device work."""
     import ctypes
 
     import bench
     want = {
         "conv1": ("v3", "c1", "c1"),
-        "layer1.0.conv1": ("fwd5", "r6", "r6"),
+        "layer1.0.conv1": ("fwd5", "gx5", "gw5"),
         "layer2.0.conv1": ("fwd5", "v7", "gw5"),  # stride 2: gx_v8, and gw5 at stride 2
         "layer2.0.conv2": ("fwd5", "gx5", "gw5"),
         "layer3.0.conv1": ("fwd5", "v7", "gw5"),  # stride 2: fwd5 with two output blocks per workgroup (its larger LDS budget)
         "layer3.0.conv2": ("fwd5", "fused", "fused"),
     }
-    got = {}
+    got, rec = {}, {}
     for name, c, o, h, s, nb in bench.RESNET20:
-        d = _desc(C=c, O=o, H=h, W=h, stride=(s, s), bits_w=nb, bits_a=nb, input_kind=L.CIMQ_INPUT_RAW_LSQ,
-                  lsq_qp=float(2 ** nb - 1))
-        r = (ctypes.c_int * 3)()
-        assert lib.cimq_module_route(ctypes.byref(d), r) == 0, lib.cimq_last_error()
-        got[name] = tuple(L.ROUTE_NAMES[v] for v in r)
+        for opt, out in ((0, got), (L.CIMQ_OPT_RECOMPUTE, rec)):
+            d = _desc(C=c, O=o, H=h, W=h, stride=(s, s), bits_w=nb, bits_a=nb, input_kind=L.CIMQ_INPUT_RAW_LSQ,
+                      lsq_qp=float(2 ** nb - 1), options=opt)
+            r = (ctypes.c_int * 3)()
+            assert lib.cimq_module_route(ctypes.byref(d), r) == 0, lib.cimq_last_error()
+            out[name] = tuple(L.ROUTE_NAMES[v] for v in r)
     for name, w in want.items():
         assert got[name] == w, (name, got[name])
-    # every 16-channel stride-1 layer of the benchmark recomputes its partial sums in the backward; the
-    # 32-channel ones take all three round-5 kernels
+    # every 3-bit stride-1 layer takes all three round-5 kernels by default; with the recompute option the
+    # 16-channel ones recompute their partial sums in the backward and the others are unchanged
     for name, c, o, h, s, nb in bench.RESNET20:
-        if nb == 3 and s == 1 and c == 16:
-            assert got[name] == ("fwd5", "r6", "r6"), (name, got[name])
-        if nb == 3 and s == 1 and c == 32:
+        if nb == 3 and s == 1 and c in (16, 32):
             assert got[name] == ("fwd5", "gx5", "gw5"), (name, got[name])
+        want_rec = ("fwd5", "r6", "r6") if (nb == 3 and s == 1 and c == 16) else got[name]
+        assert rec[name] == want_rec, (name, rec[name])
+    d = _desc(options=2)
+    assert lib.cimq_module_route(ctypes.byref(d), (ctypes.c_int * 3)()) == L.CIMQ_EINVAL  # unknown option bit
 
 
 def test_module_ctx_without_state_words(lib):
-    """ABI 13: the module entry points' ctx (cimq_sizes.module_ctx_bytes) holds no per-partial-sum state words
-    where their backward recomputes the partial sums -- 33.5 MB less per 16-channel ResNet-20 layer at B = 256 --
-    and is the Function path's ctx elsewhere."""
+    """ABI 13/14: with CIMQ_OPT_RECOMPUTE the module entry points' ctx (cimq_sizes.module_ctx_bytes) holds no
+    per-partial-sum state words where their backward recomputes the partial sums -- 33.5 MB less per 16-channel
+    ResNet-20 layer at B = 256 -- and is the Function path's ctx elsewhere and without the option."""
     import ctypes
     for (c, h, s, nb, recompute) in [(16, 32, 1, 3, True), (32, 16, 1, 3, False), (16, 32, 2, 3, False),
                                       (3, 32, 1, 8, False)]:
-        d = _desc(B=256, C=c, O=16 if c == 3 else c * s, H=h, W=h, stride=(s, s), bits_w=nb, bits_a=nb,
-                  input_kind=L.CIMQ_INPUT_RAW_LSQ, lsq_qp=float(2 ** nb - 1))
-        sz = L.Sizes()
-        assert lib.cimq_query_sizes(ctypes.byref(d), ctypes.byref(sz)) == 0, lib.cimq_last_error()
-        if recompute:
-            assert sz.ctx_bytes - sz.module_ctx_bytes >= 2 * 256 * 32 * 32 * 16 * 4  # T * M * O * 4 bytes
-        else:
-            assert sz.module_ctx_bytes == sz.ctx_bytes
+        for opt in (0, L.CIMQ_OPT_RECOMPUTE):
+            d = _desc(B=256, C=c, O=16 if c == 3 else c * s, H=h, W=h, stride=(s, s), bits_w=nb, bits_a=nb,
+                      input_kind=L.CIMQ_INPUT_RAW_LSQ, lsq_qp=float(2 ** nb - 1), options=opt)
+            sz = L.Sizes()
+            assert lib.cimq_query_sizes(ctypes.byref(d), ctypes.byref(sz)) == 0, lib.cimq_last_error()
+            if recompute and opt:
+                assert sz.ctx_bytes - sz.module_ctx_bytes >= 2 * 256 * 32 * 32 * 16 * 4  # T * M * O * 4 bytes
+            else:
+                assert sz.module_ctx_bytes == sz.ctx_bytes

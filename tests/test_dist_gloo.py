@@ -83,21 +83,32 @@ def _segment_worker(rank, world, port, out):
         from cim_quantization_amd.dist import GradBucket
         torch.manual_seed(7)
         params = [torch.nn.Parameter(torch.zeros(n)) for n in (1000, 1, 333, 4096, 17, 1)]
-        seg, one = GradBucket(params), GradBucket(params)
+        seg, one, rev = GradBucket(params), GradBucket(params), GradBucket(params)
         g = torch.Generator().manual_seed(31 + rank)
         vals = torch.randn(seg.flat.numel(), generator=g) * torch.logspace(-6, 3, seg.flat.numel()).flip(0)
         seg.flat.copy_(vals)
         one.flat.copy_(vals)
+        rev.flat.copy_(vals)
         # three segments in bucket order (bench.Trainer's layer-segment cut), the rest by exchange()
         for hi in (1001, 1334, 5430):
             seg.exchange_segment(hi)
         seg.exchange_segment(1001)  # a segment already sent is a no-op
         seg.exchange()
         one.exchange()
+        # reverse order (a network's backward finishes its last layers first): suffix ranges
+        rev.exchange_range(*rev.span(params[4:]))
+        rev.exchange_range(*rev.span(params[3:4]))
+        errs = []
+        for bad in ((5430, 5448), (1000, 1002), (0, 1001)):  # overlapping / off a boundary / fine
+            try:
+                rev.exchange_range(*bad)
+            except ValueError:
+                errs.append(bad)
+        rev.exchange()  # sends the gap [1001, 1334), waits, scales
         gathered = [torch.zeros_like(vals) for _ in range(world)]
         dist.all_gather(gathered, vals)
         out[rank] = (torch.equal(seg.flat, one.flat), float((one.flat - sum(gathered) / world).abs().max()),
-                     len(seg._works), seg._sent)
+                     len(seg._works), seg._sent, torch.equal(rev.flat, one.flat), errs, len(rev._ranges))
     finally:
         dist.destroy_process_group()
 
@@ -108,8 +119,9 @@ def test_segmented_exchange_bit_identical_world2_gloo():
     out while the next segment computes) gives the single-bucket exchange bit for bit at two ranks."""
     out = _run(_segment_worker)
     for rank in (0, 1):
-        same, err, works, sent = out[rank]
+        same, err, works, sent, same_rev, errs, ranges = out[rank]
         assert same and err == 0.0 and works == 0 and sent == 0, out[rank]
+        assert same_rev and ranges == 0 and errs == [(5430, 5448), (1000, 1002)], out[rank]
 
 
 def _broadcast_worker(rank, world, port, out):

@@ -5,8 +5,11 @@
   (fused LSQ quantisers, ``cimq_module_forward/backward``, the kernels bench.py times), against
   the module oracle on the FULL batch: out, grad_x, grad_w, grad_alpha_cim, grad_alpha_act,
   grad_alpha_weight.  The ADC codes and STE-pass bits that the production forward
-  (cim_fwd_v3_kernel) wrote into its state words are decoded and compared with the oracle's,
-  element by element, on sampled images.
+  (cim_fwd5_kernel; cim_fwd_v3_kernel on the first conv) wrote into its state words are decoded and
+  compared with the oracle's, element by element, on sampled images.  ``layer1_recompute`` runs the
+  16-channel layer with CIMQ_OPT_RECOMPUTE (no state words; cim_bwd_r6_kernel recomputes the partial
+  sums): the codes / pass bits there are the ones the recomputing backward derives, through its
+  debug instantiation (cimq_debug_recompute_codes).
 * QuantLinear 1024->1024 w4a4, 128-row tiles (BASELINE cfg5, ``Conv2dLSQCiM`` with k = 1, SURVEY
   section 0): the module at batch 4096 against the oracle on 64 sampled rows (out, grad_x), every
   integer partial sum and ADC output bit-exact, and all gradients against the module oracle on a
@@ -38,6 +41,7 @@ RESNET20_SHAPES = [
     ("layer2", 32, 32, 16, 1, 3),
     ("layer3.0.conv1_s2", 32, 64, 16, 2, 3),
     ("layer3", 64, 64, 8, 1, 3),
+    ("layer1_recompute", 16, 16, 32, 1, 3),  # CIMQ_OPT_RECOMPUTE: cim_bwd_r6_kernel
 ]
 
 
@@ -130,6 +134,7 @@ def test_resnet20_layer_module_fullbatch(cuda_device, monkeypatch, shape):
     rng = np.random.default_rng(sum(map(ord, name)))
     torch.manual_seed(0)
     m = my_nn.Conv2dLSQCiM(C, O, 3, s, 1, bias=False, **_kw(bits)).to(cuda_device)
+    m.recompute_psum = name.endswith("_recompute")
     om = cmo.OracleConv2dLSQCiM(C, O, (3, 3), (s, s), (1, 1), (1, 1), bias=False, **_kw(bits))
     om.debug_retain = True
     w = (rng.standard_normal((O, C, 3, 3)) * math.sqrt(2.0 / (9 * C))).astype(np.float32)
@@ -159,9 +164,9 @@ def test_resnet20_layer_module_fullbatch(cuda_device, monkeypatch, shape):
 
     xt = torch.from_numpy(x).to(cuda_device).requires_grad_(True)
     out = m(xt)
-    # what cim_fwd_v3_kernel recorded, before the backward (the w8a8 first conv records nothing: its
-    # backward recomputes the partial sums, cimq_c1.hip; its integer decisions are checked below on
-    # the debug forward instead)
+    # what cim_fwd5_kernel recorded, before the backward (with the recompute option, what the recomputing
+    # backward derives; the w8a8 first conv records nothing: its backward recomputes the partial sums,
+    # cimq_c1.hip; its integer decisions are checked below on the debug forward instead)
     code, passed = (None, None) if signed else F.debug_state_codes(out)
     out.backward(torch.from_numpy(g).to(cuda_device))
     torch.cuda.synchronize()

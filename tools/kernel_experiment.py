@@ -51,6 +51,18 @@ VARIANTS = {
     "gx5_noaread": ["CIMQ_EXP_GX5_NOAREAD"],
     "gx5_nomfma": ["CIMQ_EXP_GX5_NOMFMA"],
     "gx5_noaread_nomfma": ["CIMQ_EXP_GX5_NOAREAD", "CIMQ_EXP_GX5_NOMFMA"],
+    # round 6: the recompute backward (cimq_r6.hip) without its phase-A MFMAs / G writes / gw MFMAs / gx MFMAs /
+    # finish (exchange rows, act-LSQ backward, gx stores)
+    "r6_noa": ["CIMQ_EXP_R6_NOA"],
+    "r6_nog": ["CIMQ_EXP_R6_NOG"],
+    "r6_nogw": ["CIMQ_EXP_R6_NOGW"],
+    "r6_nogx": ["CIMQ_EXP_R6_NOGX"],
+    "r6_nofin": ["CIMQ_EXP_R6_NOFIN"],
+    "r6_nogwgx": ["CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX"],
+    "r6_wfpf": ["CIMQ_EXP_R6_WFPF"],  # the next tile's weight fragments prefetched
+    "r6_xfpf": ["CIMQ_EXP_R6_XFPF"],  # the finished rows' x prefetched
+    "r6_pf": ["CIMQ_EXP_R6_WFPF", "CIMQ_EXP_R6_XFPF"],
+    "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in os.environ["CIMQ_EXP_VARIANTS"].split(",")}
