@@ -43,6 +43,8 @@ PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD-32 x 2.4 GHz (a wa
 # grad_w + the parameter-gradient epilogue on a second stream (CIMQ_BENCH_OVERLAP=0: one stream,
 # the epilogues of all layers packed into a few launches at the end of the backward)
 OVERLAP = os.environ.get("CIMQ_BENCH_OVERLAP", "0") == "1"
+# CIMQ_BENCH_RECOMPUTE=1: the layers run with Conv2dLSQCiM.recompute_psum (CIMQ_OPT_RECOMPUTE)
+RECOMPUTE = os.environ.get("CIMQ_BENCH_RECOMPUTE", "0") == "1"
 TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r05_final", "pmc_traffic.json"))
 # the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
 # prefixes (the keys of pmc_traffic.json); every launch of a family is timed, all its instantiations
@@ -69,6 +71,7 @@ def build(device, batch, seed=0, data_seed=None):
         m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
                                abitslice=1, xbar=XBAR, adcbits=ADC, signed_xbar=True, stochastic_quant=False)
         torch.nn.init.kaiming_normal_(m.weight)
+        m.recompute_psum = RECOMPUTE
         layers.append(m.to(device).train())
         x = torch.randn(batch, c, h, h, generator=gen)
         if name != "conv1":
@@ -487,6 +490,9 @@ def bench_layers(dev, specs, batch, xbar, adc, steps, warmup, adc_shift=False, r
     first-step alpha init runs in the warm-up), logical MAC/s as SURVEY 8(d) defines it."""
     import cim_quantization_amd._modules as my_nn
     torch.manual_seed(11)
+    torch.cuda.synchronize(dev)
+    mem0 = torch.cuda.memory_allocated(dev)  # what earlier configs still hold
+    torch.cuda.reset_peak_memory_stats(dev)
     layers, xs, gs, macs = [], [], [], 0
     for name, c, o, h, s, nb in specs:
         m = my_nn.Conv2dLSQCiM(c, o, 3, s, 1, bias=False, nbits_w=nb, nbits_a=nb, nbits_alpha=8, wbitslice=1,
@@ -511,6 +517,7 @@ def bench_layers(dev, specs, batch, xbar, adc, steps, warmup, adc_shift=False, r
         fb()
     torch.cuda.synchronize(dev)
     t_fb = (time.perf_counter() - t0) / steps
+    peak_mb = (torch.cuda.max_memory_allocated(dev) - mem0) / 2 ** 20
     with torch.no_grad():
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -519,7 +526,8 @@ def bench_layers(dev, specs, batch, xbar, adc, steps, warmup, adc_shift=False, r
         torch.cuda.synchronize(dev)
     t_f = (time.perf_counter() - t0) / steps
     out = {"ms_fwd_bwd": t_fb * 1e3, "ms_fwd": t_f * 1e3, "fwd_mac_per_s": macs / t_f, "launch": "eager",
-           "layers": len(specs), "batch": batch}
+           "layers": len(specs), "batch": batch,
+           "peak_mem_mb": round(peak_mb, 1)}  # device memory this stack's inputs, parameters and fwd+bwd peaked at
     # the same fwd+bwd replayed as one HIP graph: device time without the host's per-launch cost
     # (eager timings of these many-small-launch stacks move with the box's host load)
     try:
@@ -573,6 +581,7 @@ def main():
     from cim_quantization_amd import _lib
     _lib.load()  # fail loudly if the HIP library is missing
 
+    torch.cuda.reset_peak_memory_stats(dev)
     layers, xs, gs = build(dev, args.batch, seed=1234, data_seed=1235 + 1000 * rank)
     tr = Trainer(layers, world)
     for _ in range(max(1, args.warmup)):  # the first step runs the LSQ / alpha_cim init (lsq.py:532-563)
@@ -607,6 +616,8 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, fwd_elapsed = t.tolist()
+    # device memory of the whole training step (inputs, parameters, bucket, ctx / workspaces, the graph's pool)
+    peak_mb = torch.cuda.max_memory_allocated(dev) / 2 ** 20
     breakdown = layer_breakdown(tr, xs, gs, dev)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -645,9 +656,10 @@ def main():
         "config": {"workload": "resnet20_w3a3_all_19_cim_convs_fwd_bwd_sgd", "global_batch": args.batch * world,
                    "per_gpu_batch": args.batch, "xbar": XBAR, "adc_bits": ADC, "first_layer": "w8a8",
                    "parallelism": f"dp{world}", "grad_bucket_mb": round(tr.bucket_mb, 3), "exchange_segments": len(tr.segments),
-                   "launch": "hip_graph" if graph else "eager"},
+                   "launch": "hip_graph" if graph else "eager", "recompute_psum": RECOMPUTE},
         "roofline": dict(roof, kernel=_lib.KERNEL_SYMBOLS[_lib.KERNEL_IDS[dominant]] + " (every instantiation the "
                          "19 layers launch)", avg_launch_us=kt.total_ms / nl * 1e3, pmc_source=pmc_source),
+        "peak_mem_mb": round(peak_mb, 1),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in per_kernel.items()},
         "layer_fwd_bwd_ms": breakdown,
         "rates": step_context(args.batch, world, ms_per_step, fwd_elapsed / args.steps * 1e3),

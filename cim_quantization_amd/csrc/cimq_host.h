@@ -414,9 +414,10 @@ inline Plan7 v7_plan(const Geo& g) {
   else if (128 % g.P == 0) v.whole = 1;
   else return p;
   v.lw = p3.v.lw;
-  // input rows per band: 16 (round 5, once only the stride-2 layers of the benchmark still ran this kernel:
-  // 105.7 -> 80.6 us/step for ResNet-20's two; 8 and 32 slower, gpurun_out/r05_sw7, r05_sw8)
-  v.RB = std::min(g.H, tune("GX_RB", 16));
+  // input rows per band, per shape: 16 at stride 2 (round 5: 105.7 -> 80.6 us/step for ResNet-20's two
+  // downsampling layers; 8 and 32 slower, gpurun_out/r05_sw7, r05_sw8), 8 at stride 1 (the w2a2 ResNet-56
+  // layers and the xbar-64 single conv: 16-row bands made them 6-33 % slower, halving the blocks at B = 4)
+  v.RB = std::min(g.H, tune("GX_RB", g.SH == 2 ? 16 : 8));
   v.nbands = (g.H + v.RB - 1) / v.RB;
   v.FBX = g.FBT;
   // grad_x v8: (c, kh)-row blocks per tile, ring of output rows

@@ -243,7 +243,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
   };
 
   const int nmt = v.nmt;
-#ifdef CIMQ_EXP_R6_WFPF
+#ifndef CIMQ_EXP_R6_NO_WFPF
   v4i wnx[9];  // the next tile's forward weight fragments, in flight one tile ahead
 #pragma unroll
   for (int q = 0; q < 9; ++q) wnx[q] = wf5[(size_t)v.tc0[0] * 9 * 64 + lane + q * 64];
@@ -272,7 +272,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     for (int i = 0; i < T; ++i) {
       // the tile's forward weight fragments [s][k] (cim_fwd5_kernel's operand, output block 0)
       v4i wfr[9];
-#ifdef CIMQ_EXP_R6_WFPF
+#ifndef CIMQ_EXP_R6_NO_WFPF
       {
         const v4i* wt = wf5 + (size_t)v.tc0[i + 1 < T ? i + 1 : 0] * 9 * 64 + lane;
 #pragma unroll
@@ -414,7 +414,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
     }
     __syncthreads();  // (B1) the G patch is complete; the patches' readers are done
     if (more) stage_store(r0 + R, xv);  // the next m-tile's patches (its phase A reads them after B4)
-#ifdef CIMQ_EXP_R6_XFPF
+#ifndef CIMQ_EXP_R6_NO_XFPF
     float4 xf[2];  // the finished rows' x (act-LSQ backward), in flight behind the gx MFMAs
     {
       const int t = (int)threadIdx.x;
@@ -477,7 +477,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
       float4* ca = reinterpret_cast<float4*>(smem + O_CA);
       auto fin = [&](int ih, float4 v4, int u) {
         const int gi = ((b * C + c) * H + ih) * W + iw;
-#ifdef CIMQ_EXP_R6_XFPF
+#ifndef CIMQ_EXP_R6_NO_XFPF
         const float4 xv4 = xf[u];
 #else
         (void)u;

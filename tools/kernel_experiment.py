@@ -59,9 +59,7 @@ VARIANTS = {
     "r6_nogx": ["CIMQ_EXP_R6_NOGX"],
     "r6_nofin": ["CIMQ_EXP_R6_NOFIN"],
     "r6_nogwgx": ["CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX"],
-    "r6_wfpf": ["CIMQ_EXP_R6_WFPF"],  # the next tile's weight fragments prefetched
-    "r6_xfpf": ["CIMQ_EXP_R6_XFPF"],  # the finished rows' x prefetched
-    "r6_pf": ["CIMQ_EXP_R6_WFPF", "CIMQ_EXP_R6_XFPF"],
+    "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
 }
 if os.environ.get("CIMQ_EXP_VARIANTS"):
