@@ -416,8 +416,12 @@ inline Plan7 v7_plan(const Geo& g) {
   v.lw = p3.v.lw;
   // input rows per band, per shape: 16 at stride 2 (round 5: 105.7 -> 80.6 us/step for ResNet-20's two
   // downsampling layers; 8 and 32 slower, gpurun_out/r05_sw7, r05_sw8), 8 at stride 1 (the w2a2 ResNet-56
-  // layers and the xbar-64 single conv: 16-row bands made them 6-33 % slower, halving the blocks at B = 4)
-  v.RB = std::min(g.H, tune("GX_RB", g.SH == 2 ? 16 : 8));
+  // layers and the xbar-64 single conv: 16-row bands made them 6-33 % slower), halved while the grid has fewer
+  // blocks than the chip has CUs (cfg1, B = 4: 16 -> 128 bands, 0.138 / 0.107 -> 0.108 / 0.077 ms per fwd+bwd,
+  // gpurun_out/r06_rb)
+  int rb = g.SH == 2 ? 16 : 8;
+  while (rb > 1 && (long long)g.B * cdiv(g.H, rb) < 256) rb /= 2;
+  v.RB = std::min(g.H, tune("GX_RB", rb));
   v.nbands = (g.H + v.RB - 1) / v.RB;
   v.FBX = g.FBT;
   // grad_x v8: (c, kh)-row blocks per tile, ring of output rows
