@@ -124,7 +124,12 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     const int sl = pw / PI, pin0 = pw - sl * PI;  // image slot, pixel within the slot
     const int b = b0 + sl;
     float4 gq;
+#ifdef CIMQ_EXP_GW5_NOLOAD  // attribution builds only: no global reads in the m-tile loop (wrong results)
+    gq = make_float4(1e-3f * o, 2e-3f, 3e-3f * mt, 4e-3f);
+    if (false) {
+#else
     if (g.onchw) {
+#endif
       gq = *reinterpret_cast<const float4*>(gout + ((size_t)b * g.O + o) * g.P + p0 + pin0);
     } else {  // the Function path's [B, P, O]
       const float* gp = gout + ((size_t)b * g.P + p0 + pin0) * g.O + o;
@@ -136,7 +141,12 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sq[q][e] = q < ntl ? st[((size_t)(i_lo + q) * g.M + m + e) * g.O + o] : 0u;
+        for (int e = 0; e < 4; ++e)
+#ifdef CIMQ_EXP_GW5_NOLOAD
+          sq[q][e] = (uint32_t)(m * 2654435761u + e * 40503u + o) & 0x7FFFFFFu;
+#else
+          sq[q][e] = q < ntl ? st[((size_t)(i_lo + q) * g.M + m + e) * g.O + o] : 0u;
+#endif
     }
     // A-ready patch: input rows oh0 * SH - 1 .. (oh0 + R - 1) * SH + 1 of each image slot, the block's 16
     // channels; item = (c, slot, row, col) (W a power of two; the divisions by RH and CH as exact
@@ -161,7 +171,11 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
             const int xi = xb + (slt * g.C + c) * HWi + row * g.W + col;
             // (a code byte, expanded below through the LDS table, or the word itself)
             // (unsigned offsets: the loads take the scalar base + 32-bit offset form)
+#ifdef CIMQ_EXP_GW5_NOLOAD
+            wv[u] = CODES ? (uint32_t)(xi & 7) : (uint32_t)xi * 0x010203u;
+#else
             wv[u] = CODES ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[(uint32_t)xi] : xcb[(uint32_t)xi];
+#endif
           }
         }
       }
@@ -204,7 +218,11 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       for (int q = 0; q < 2; ++q) {
         if (q >= ntl) break;
         const uint32_t s0 = sq[q][e0], s1 = sq[q][e0 + 1];
+#ifdef CIMQ_EXP_GW5_NOGA
+        if (false) {
+#else
         if (own[q]) {
+#endif
           // grad_alpha partials (lsq.py:321-333): code * g, the code the signed 2-bit field at bit 3kj + 1
 #pragma unroll
           for (int kj = 0; kj < 9; ++kj) {
@@ -241,6 +259,10 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
           const int ao = (int)((aoffp[fb >> 1] >> (16 * (fb & 1))) & 0xFFFFu);
           const uint2 a0 = pat[ao + poff], a1 = pat[ao + poff + SS];
           const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
+#ifdef CIMQ_EXP_GW5_NOMFMA
+          acc[fb][0] += (float)a[0] + (float)bh[0] + (float)bm[1] + (float)bl[2];
+          continue;
+#endif
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
           acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
@@ -250,6 +272,20 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   }
 
   // the block's part of its chunk's slab: the 8 waves summed in LDS in wave order
+#ifdef CIMQ_EXP_GW5_NOEPI
+  {
+    float* gws = gw_slab + (size_t)blockIdx.x * g.T * g.FBT * 16 * g.Opad;
+    float t = 0.f;
+#pragma unroll
+    for (int fb = 0; fb < 9; ++fb) t += acc[fb][0] + acc[fb][1] + acc[fb][2] + acc[fb][3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int kj = 0; kj < 9; ++kj) t += ga[q][kj];
+    gws[threadIdx.x] = t;
+    return;
+  }
+#endif
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);  // [8 waves][64 lanes][4]
   const size_t rows = (size_t)g.T * g.FBT * 16;

@@ -55,6 +55,30 @@ inline int tune(const char* name, int dflt) {
 #else
 constexpr int tune(const char*, int dflt) { return dflt; }
 #endif
+// Host plans and layouts memoised per geometry (the launch paths ask for the same ones several times per call):
+// a few recent Geo values per thread, compared bytewise with the fields no plan reads (the prepared-weight
+// pointer, the stochastic-ADC key) cleared.  Padding can only cause a miss, never a wrong hit.
+template <class T, T (*F)(const Geo&)>
+inline T memo_geo(const Geo& g) {
+  struct Entry {
+    Geo k;
+    T v;
+    bool used;
+  };
+  thread_local Entry e[4] = {};
+  thread_local int next = 0;
+  Geo k = g;
+  k.wbase = nullptr;
+  k.seed_lo = k.seed_hi = 0;
+  for (Entry& x : e)
+    if (x.used && memcmp(&x.k, &k, sizeof(Geo)) == 0) return x.v;
+  Entry& d = e[next];
+  next = (next + 1) & 3;
+  d.v = F(g);
+  d.k = k;
+  d.used = true;
+  return d.v;
+}
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 inline int make_geo(const cimq_conv_desc* d, Geo* out) {
@@ -171,7 +195,7 @@ inline size_t x5_frag_bytes(const Geo& g);  // after x5_plan
 inline size_t r6_frag_bytes(const Geo& g);  // after r6_plan
 inline bool r6_bwd(const Geo& g);           // after r6_plan
 
-inline CtxLayout ctx_layout(const Geo& g) {
+inline CtxLayout ctx_layout_compute(const Geo& g) {
   CtxLayout L;
   size_t o = 0;
   const size_t npar = (size_t)g.T * g.nba * g.nbw * g.Opad;
@@ -210,6 +234,7 @@ inline CtxLayout ctx_layout(const Geo& g) {
   L.total = o;
   return L;
 }
+inline CtxLayout ctx_layout(const Geo& g) { return memo_geo<CtxLayout, ctx_layout_compute>(g); }
 
 // base of the weight-side regions of a ctx: the prepared buffer when the call has one
 inline uint8_t* wreg(const Geo& g, const uint8_t* ctx) {
@@ -392,7 +417,7 @@ inline void gw_pitches(const Geo& g, V7& v) {
   v.KWP = it->second.second;
 }
 
-inline Plan7 v7_plan(const Geo& g) {
+inline Plan7 v7_plan_compute(const Geo& g) {
   Plan7 p;
   memset(&p, 0, sizeof(p));
 #ifdef CIMQ_NO_V7
@@ -478,6 +503,7 @@ inline Plan7 v7_plan(const Geo& g) {
   p.ok = p.lds_gx <= lim && p.lds_gw <= lim;
   return p;
 }
+inline Plan7 v7_plan(const Geo& g) { return memo_geo<Plan7, v7_plan_compute>(g); }
 
 // ---- the fused backward (cimq_fused.hip): one kernel per stride-1 3x3 w2a2 / w3a3 layer ----
 struct Plan9 {
@@ -544,7 +570,7 @@ inline void fused_pitches(const Geo& g, V9& v) {
   v.KWP = it->second.second;
 }
 
-inline Plan9 v9_plan(const Geo& g) {
+inline Plan9 v9_plan_compute(const Geo& g) {
   Plan9 p;
   memset(&p, 0, sizeof(p));
   if (tune("FUSED", 1) == 0) return p;
@@ -595,6 +621,7 @@ inline Plan9 v9_plan(const Geo& g) {
   p.ok = o <= kLdsMax - 512;
   return p;
 }
+inline Plan9 v9_plan(const Geo& g) { return memo_geo<Plan9, v9_plan_compute>(g); }
 
 // ---- the first conv's backward from recomputed partial sums (cimq_c1.hip) ----
 struct PlanC1 {
@@ -720,7 +747,7 @@ struct Plan5 {
   int nob;  // 16-channel output blocks per workgroup (the kernel's template argument)
 };
 
-inline Plan5 f5_plan(const Geo& g) {
+inline Plan5 f5_plan_compute(const Geo& g) {
   Plan5 p;
   memset(&p, 0, sizeof(p));
   if (tune("FWD5", 1) == 0) return p;
@@ -794,6 +821,7 @@ inline Plan5 f5_plan(const Geo& g) {
   p.ok = p.lds <= budget;
   return p;
 }
+inline Plan5 f5_plan(const Geo& g) { return memo_geo<Plan5, f5_plan_compute>(g); }
 // wf5 fragments of a layer (all output-channel blocks)
 inline size_t f5_frag_items(const Geo& g, const Plan5& p) { return p.ok ? (size_t)g.OB16 * p.v.ntc * 9 * 64 : 0; }
 inline size_t f5_frag_bytes(const Geo& g) { return f5_frag_items(g, f5_plan(g)) * 16; }
@@ -806,7 +834,7 @@ struct PlanG5 {
   int pairs;  // (input, output) 16-channel block pairs: grid y
 };
 
-inline PlanG5 g5_plan(const Geo& g) {
+inline PlanG5 g5_plan_compute(const Geo& g) {
   PlanG5 p;
   memset(&p, 0, sizeof(p));
   if (tune("GW5", 1) == 0) return p;
@@ -851,6 +879,7 @@ inline PlanG5 g5_plan(const Geo& g) {
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }
+inline PlanG5 g5_plan(const Geo& g) { return memo_geo<PlanG5, g5_plan_compute>(g); }
 
 // ---- grad_x of the w3a3 stride-1 16 -> 16 (32 x 32) / 32 -> 32 (16 x 16) layers, per input pixel (cimq_gx5.hip) ----
 struct PlanX5 {
@@ -860,7 +889,7 @@ struct PlanX5 {
   int nblk;  // grid = the d sa partials it leaves
 };
 
-inline PlanX5 x5_plan(const Geo& g) {
+inline PlanX5 x5_plan_compute(const Geo& g) {
   PlanX5 p;
   memset(&p, 0, sizeof(p));
   if (tune("GX5", 1) == 0) return p;
@@ -885,6 +914,7 @@ inline PlanX5 x5_plan(const Geo& g) {
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }
+inline PlanX5 x5_plan(const Geo& g) { return memo_geo<PlanX5, x5_plan_compute>(g); }
 inline size_t x5_frag_bytes(const Geo& g) {
   const PlanX5 p = x5_plan(g);
   return p.ok ? (size_t)g.T * p.v.CBN * 9 * 2 * p.v.CBN * 64 * 16 : 0;
@@ -897,7 +927,7 @@ struct PlanR6 {
   size_t lds;
 };
 
-inline PlanR6 r6_plan(const Geo& g) {
+inline PlanR6 r6_plan_compute(const Geo& g) {
   PlanR6 p;
   memset(&p, 0, sizeof(p));
   if (!g.recompute || tune("R6", 1) == 0) return p;  // the caller's choice (CIMQ_OPT_RECOMPUTE)
@@ -918,6 +948,7 @@ inline PlanR6 r6_plan(const Geo& g) {
   p.ok = true;
   return p;
 }
+inline PlanR6 r6_plan(const Geo& g) { return memo_geo<PlanR6, r6_plan_compute>(g); }
 inline size_t r6_frag_bytes(const Geo& g) { return r6_plan(g).ok ? (size_t)kR6WxItems * 16 : 0; }
 // decided at launch: the module entry points (g.onchw) run cim_fwd5_kernel, whose operand the recompute needs; the
 // Function path's forward writes state words and keeps the state-word backward
@@ -944,7 +975,7 @@ inline int shift_chunks(const Geo& g) {
   return std::max(1, std::min(per, g.M / 64));
 }
 
-inline WsLayout ws_layout(const Geo& g) {
+inline WsLayout ws_layout_compute(const Geo& g) {
   WsLayout W;
   gw_chunks(g, &W.rows, &W.nchunks);
   // backward slabs: the v7 grad_w kernel's pixel chunks when it applies (the alpha_cim init
@@ -983,6 +1014,7 @@ inline WsLayout ws_layout(const Geo& g) {
   W.total = o;
   return W;
 }
+inline WsLayout ws_layout(const Geo& g) { return memo_geo<WsLayout, ws_layout_compute>(g); }
 
 template <typename K>
 inline int set_lds(K kernel, size_t bytes) {

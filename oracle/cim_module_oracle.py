@@ -150,3 +150,32 @@ class OracleConv2dLSQCiM(torch.nn.Conv2d):
         if self.bias is not None:
             out = out + self.bias
         return out
+
+
+def alpha_cim_terms(alpha, aa, nbits_alpha=8):
+    """Checker helper: per-entry sum of |terms| of grad alpha_cim through the alpha quantiser (lsq.py:566-571).
+
+    alpha_q_e = clamp(round_pass(alpha_e / scale), 1, Qp) * scale with scale = (max - min) / (Qp - 1), so
+    d loss / d alpha_f = G_f * pass_f + ([f is the max] - [f is the min]) / (Qp - 1) * sum_e G_e * (r_e - pass_e * v_e)
+    (G = d loss / d alpha_q, v = alpha / scale, r its clamped code, pass the clamp mask of rint(v); tied extrema share
+    the scale gradient).  ``aa`` is the oracle's fp64 sum of |terms| of G per entry (cim_backward absolute=True), so
+    an entry's terms are aa_f * pass_f plus, on the max / min entries, sum_e aa_e * (r_e + pass_e |v_e|) / (Qp - 1):
+    the exact first-order error bound of the fp32 sums.  All-equal alpha (scale 0: v infinite or NaN, no entry
+    passes) gives every entry the edge form with finite terms."""
+    a32 = np.asarray(alpha, np.float32)
+    a = a32.astype(np.float64)
+    aa = np.broadcast_to(np.asarray(aa, np.float64), a.shape)
+    qp = 2 ** nbits_alpha - 1
+    # the clamp's pass mask is decided on the ROUNDED value (clamp(round_pass(v), 1, Qp): its input is rint(v)), in
+    # fp32 as the module computes it
+    sc32 = (a32.max() - a32.min()) / np.float32(qp - 1)
+    with np.errstate(all="ignore"):
+        v32 = (a32 / sc32).astype(np.float32)
+    rv = np.rint(v32).astype(np.float64)
+    passed = (rv >= 1) & (rv <= qp)
+    vabs = np.where(passed, np.abs(v32.astype(np.float64)), 0.0)
+    r = np.nan_to_num(np.clip(rv, 1, qp), nan=float(qp))
+    t = aa * passed
+    edge = (a == a.max()) | (a == a.min())
+    return np.where(edge, aa + (aa * (r + vabs)).sum() / (qp - 1), t)
+

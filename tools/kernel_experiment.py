@@ -59,6 +59,11 @@ VARIANTS = {
     "r6_nogx": ["CIMQ_EXP_R6_NOGX"],
     "r6_nofin": ["CIMQ_EXP_R6_NOFIN"],
     "r6_nogwgx": ["CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX"],
+    "gw5_noload": ["CIMQ_EXP_GW5_NOLOAD"],  # gw5 without its global reads (timing only)
+    "gw5_noga": ["CIMQ_EXP_GW5_NOGA"],
+    "gw5_nomfma": ["CIMQ_EXP_GW5_NOMFMA"],
+    "gw5_noepi": ["CIMQ_EXP_GW5_NOEPI"],
+    "gw5_skel": ["CIMQ_EXP_GW5_NOLOAD", "CIMQ_EXP_GW5_NOGA", "CIMQ_EXP_GW5_NOMFMA", "CIMQ_EXP_GW5_NOEPI"],
     "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
 }
