@@ -76,7 +76,11 @@ __device__ inline void dense_fwd_body(const Geo& g, const uint8_t* __restrict__ 
   // out accumulators of the four channel blocks in LDS ([wave][ob][lane]); one block's in registers
   float4* acc_l = accs + wave * 4 * 64 + lane;
   for (int i = 0; i < g.T; ++i) {
+#ifdef CIMQ_EXP_DENSE_NOPRM
+    if (!LIT && i == 0) {
+#else
     if (!LIT) {
+#endif
       __syncthreads();
       for (int t = threadIdx.x; t < NKJ * 64; t += 256) {
         const int col = t & 63, jk = t >> 6, j = jk / NBW, k = jk - j * NBW;
@@ -145,7 +149,12 @@ __device__ inline void dense_fwd_body(const Geo& g, const uint8_t* __restrict__ 
             const int4 pv = prm[pcol];
             const float cf = cfl[pcol];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) adc_ps(ps[j][r], pv, cf, acc[r], sp[r], sz[r], sn[r]);
+            for (int r = 0; r < 4; ++r)
+#ifdef CIMQ_EXP_DENSE_NOADC  // attribution builds only (tools/kernel_experiment.py): wrong results
+              acc[r] += (float)ps[j][r] * cf + (float)pv.x;
+#else
+              adc_ps(ps[j][r], pv, cf, acc[r], sp[r], sz[r], sn[r]);
+#endif
           } else {
             // degenerate alpha / scales: the literal ADC per partial sum (as cim_fwd_v3_kernel)
             const int o = og * 64 + ob * 16 + r16;
@@ -170,7 +179,11 @@ __device__ inline void dense_fwd_body(const Geo& g, const uint8_t* __restrict__ 
         const size_t m = (size_t)m0 + wave * 16 + 4 * g4 + r;
         // code fields: lo -> 11, hi -> 01 (lo wins, as the ADC's second select)
         const uint32_t code = spread16(sz[r] | sn[r]) | (spread16(sn[r]) << 1);
+#ifndef CIMQ_EXP_DENSE_NOSTORE
         st[((size_t)i * g.M + m) * g.O + o] = make_uint2(code, sp[r] & 0xFFFFu);
+#else
+        if (code == 0x12345u) st[m] = make_uint2(code, sp[r]);
+#endif
       }
       if (i + 1 < g.T) {
         acc_l[ob * 64] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -194,6 +207,135 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void d
   if (__builtin_amdgcn_readfirstlane(pp.flags[0]) != 0) return;
   dense_fwd_body<NBW, NBA, KS, false>(g, xcf, wfrag, pp, 0.f, 0.f, out, st, prm, cfl, accs, blockIdx.x * 64,
                                       blockIdx.y);
+}
+
+// The threshold path on 128 x 64 tiles (512 threads, wave w = rows 16w..16w+15): the weight fragments
+// and the ADC / STE thresholds of a crossbar tile are staged ONCE per block into LDS and read by its eight
+// waves (the 64-row form above re-read the tile's weight fragments from L2 in every wave: 1 GB per cfg5
+// forward).  The weight fragments go in two halves (output blocks 0-1, then 2-3) so a block stays under
+// 80 KB of LDS: two blocks per CU.  Per partial sum the ADC / state bits are adc_ps, in the same order:
+// out and the state words are bit-identical to dense_fwd_kernel's.
+template <int NBW, int NBA, int KS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void dense_fwd8_kernel(
+    Geo g, const uint8_t* __restrict__ xcf, const v4i* __restrict__ wfrag, Params pp, float* __restrict__ out,
+    uint2* __restrict__ st) {
+  constexpr int NKJ = NBW * NBA;
+  constexpr int NWH = KS * NBW * 2 * 64;  // v4i of one half's weight fragments
+  __shared__ int4 prm[NKJ * 64];          // [j][k][64 channels]: thi, tlo, mlo, span
+  __shared__ float cfl[NKJ * 64];
+  __shared__ v4i wkl[NWH];                // [ks][k][2 output blocks][64 lanes]
+  __shared__ float4 accs[8 * 4 * 64];     // [wave][output block][lane]: out across the tiles
+  if (__builtin_amdgcn_readfirstlane(pp.flags[0]) != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int m0 = blockIdx.x * 128, og = blockIdx.y;
+  const int mrow = m0 + wave * 16 + r16;  // this lane's A row
+  float4* acc_l = accs + wave * 4 * 64 + lane;
+  auto stage_w = [&](int i, int half) {
+    for (int t = threadIdx.x; t < NWH; t += 512) {
+      const int l = t & 63, obh = (t >> 6) & 1, kk = t >> 7, k = kk % NBW, ks = kk / NBW;
+      wkl[t] = wfrag[((size_t)(i * KS + ks) * g.NBLK + k * g.OB16 + og * 4 + half * 2 + obh) * 64 + l];
+    }
+  };
+  for (int i = 0; i < g.T; ++i) {
+    // A operands of this wave's rows (issued first: they do not depend on the barrier)
+    uint32_t w[KS][16];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = i * g.xbar + ks * 64 + 16 * g4;
+      if (c0 < g.C) {
+        const uint4* src = reinterpret_cast<const uint4*>(xcf + ((size_t)mrow * g.C + c0) * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 t4 = src[q];
+          w[ks][4 * q] = t4.x; w[ks][4 * q + 1] = t4.y; w[ks][4 * q + 2] = t4.z; w[ks][4 * q + 3] = t4.w;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) w[ks][e] = 0u;
+      }
+    }
+    __syncthreads();  // the previous tile's readers of prm / wkl are done
+    for (int t = threadIdx.x; t < NKJ * 64; t += 512) {
+      const int col = t & 63, jk = t >> 6, j = jk / NBW, k = jk - j * NBW;
+      const int pi = pidx(g, i, j, k, og * 64 + col);
+      prm[t] = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
+      cfl[t] = pp.coef[pi];
+    }
+    stage_w(i, 0);
+    v4i xs[NBA][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t P[4];
+        tr4(w[ks][4 * q], w[ks][4 * q + 1], w[ks][4 * q + 2], w[ks][4 * q + 3], P);
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) xs[j][ks][q] = (int)P[j];
+      }
+    __syncthreads();
+#pragma unroll 1
+    for (int ob = 0; ob < 4; ++ob) {
+      if (ob == 2) {
+        __syncthreads();  // half 0 read by every wave
+        stage_w(i, 1);
+        __syncthreads();
+      }
+      float acc[4];
+      if (i == 0) {
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+      } else {
+        const float4 a4 = acc_l[ob * 64];
+        acc[0] = a4.x; acc[1] = a4.y; acc[2] = a4.z; acc[3] = a4.w;
+      }
+      uint32_t sp[4], sz[4], sn[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sp[r] = sz[r] = sn[r] = 0u;
+#pragma unroll
+      for (int k = NBW - 1; k >= 0; --k) {
+        v4i wk[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wk[ks] = wkl[((ks * NBW + k) * 2 + (ob & 1)) * 64 + lane];
+        v4i ps[NBA];
+#pragma unroll
+        for (int j = 0; j < NBA; ++j) {
+          ps[j] = v4i{0, 0, 0, 0};
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) ps[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xs[j][ks], wk[ks], ps[j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = NBA - 1; j >= 0; --j) {
+          const int pcol = (j * NBW + k) * 64 + ob * 16 + r16;
+          const int4 pv = prm[pcol];
+          const float cf = cfl[pcol];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#ifdef CIMQ_EXP_DENSE_NOADC
+            acc[r] += (float)ps[j][r] * cf + (float)pv.x;
+#else
+            adc_ps(ps[j][r], pv, cf, acc[r], sp[r], sz[r], sn[r]);
+#endif
+        }
+      }
+      const int o = og * 64 + ob * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t m = (size_t)m0 + wave * 16 + 4 * g4 + r;
+        const uint32_t code = spread16(sz[r] | sn[r]) | (spread16(sn[r]) << 1);
+#ifndef CIMQ_EXP_DENSE_NOSTORE
+        st[((size_t)i * g.M + m) * g.O + o] = make_uint2(code, sp[r] & 0xFFFFu);
+#else
+        if (code == 0x12345u) st[m] = make_uint2(code, sp[r]);
+#endif
+      }
+      if (i + 1 < g.T) {
+        acc_l[ob * 64] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[((size_t)m0 + wave * 16 + 4 * g4 + r) * g.O + o] = acc[r];
+      }
+    }
+  }
 }
 
 // Degenerate alpha_q / scales (flag set): the literal ADC per partial sum, a few blocks looping
@@ -530,13 +672,19 @@ __global__ __launch_bounds__(512) void dense_gw_kernel(Geo g, int rows_per_chunk
 template <int NBW, int NBA>
 int launch_dense_fwd_n(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s) {
   CtxLayout L = ctx_layout(g);
-  auto kern = g.KS == 1 ? dense_fwd_kernel<NBW, NBA, 1> : dense_fwd_kernel<NBW, NBA, 2>;
   auto klit = g.KS == 1 ? dense_fwd_lit_kernel<NBW, NBA, 1> : dense_fwd_lit_kernel<NBW, NBA, 2>;
   const uint8_t* wr = wreg(g, ctx);
   uint2* st = reinterpret_cast<uint2*>(ctx + L.st);
   const int slot = prof_begin(KID_FWD, g, s);
-  hipLaunchKernelGGL(kern, dim3(g.M / 64, g.O / 64), dim3(256), 0, s, g, ctx + L.xcode,
-                     reinterpret_cast<const v4i*>(wr + L.wfrag), params_of(g, ctx), sw, sa, out, st);
+  if (tune("DENSE_FWD8", 1)) {  // 128-row blocks, weight side staged once per block (dense_plan: M % 128 == 0)
+    auto kern = g.KS == 1 ? dense_fwd8_kernel<NBW, NBA, 1> : dense_fwd8_kernel<NBW, NBA, 2>;
+    hipLaunchKernelGGL(kern, dim3(g.M / 128, g.O / 64), dim3(512), 0, s, g, ctx + L.xcode,
+                       reinterpret_cast<const v4i*>(wr + L.wfrag), params_of(g, ctx), out, st);
+  } else {
+    auto kern = g.KS == 1 ? dense_fwd_kernel<NBW, NBA, 1> : dense_fwd_kernel<NBW, NBA, 2>;
+    hipLaunchKernelGGL(kern, dim3(g.M / 64, g.O / 64), dim3(256), 0, s, g, ctx + L.xcode,
+                       reinterpret_cast<const v4i*>(wr + L.wfrag), params_of(g, ctx), sw, sa, out, st);
+  }
   prof_end(slot, s);
   hipLaunchKernelGGL(klit, dim3(32), dim3(256), 0, s, g, ctx + L.xcode, reinterpret_cast<const v4i*>(wr + L.wfrag),
                      params_of(g, ctx), sw, sa, out, st);

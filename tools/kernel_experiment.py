@@ -64,6 +64,9 @@ VARIANTS = {
     "gw5_nomfma": ["CIMQ_EXP_GW5_NOMFMA"],
     "gw5_noepi": ["CIMQ_EXP_GW5_NOEPI"],
     "gw5_skel": ["CIMQ_EXP_GW5_NOLOAD", "CIMQ_EXP_GW5_NOGA", "CIMQ_EXP_GW5_NOMFMA", "CIMQ_EXP_GW5_NOEPI"],
+    "dense_noadc": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE"],  # cfg5 forward attribution (timing only)
+    "dense_nostore": ["CIMQ_EXP_DENSE_NOSTORE"],
+    "dense_noprm": ["CIMQ_EXP_DENSE_NOPRM"],
     "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
 }
