@@ -287,24 +287,29 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   }
 #endif
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [8 waves][64 lanes][4]
+  float* red = reinterpret_cast<float*>(smem);  // [8 waves][FC row blocks][64 lanes][4] (g5_plan: >= 24 KB)
   const size_t rows = (size_t)g.T * g.FBT * 16;
   float* gws = gw_slab + (size_t)blockIdx.x * rows * g.Opad;
+  // three 16-row blocks at a time: every wave stores its accumulators, then all 512 threads sum the 8 waves
+  // (in wave order, from 0: the sums of the one-wave reduction before, bit for bit) and store 16 consecutive
+  // channels per 16 threads
+  constexpr int FC = 3;
 #pragma unroll
-  for (int fb = 0; fb < 9; ++fb) {
-    reinterpret_cast<float4*>(red)[wave * 64 + lane] = make_float4(acc[fb][0], acc[fb][1], acc[fb][2], acc[fb][3]);
+  for (int c0 = 0; c0 < 9; c0 += FC) {
+#pragma unroll
+    for (int fl = 0; fl < FC; ++fl)
+      reinterpret_cast<float4*>(red)[(wave * FC + fl) * 64 + lane] =
+          make_float4(acc[c0 + fl][0], acc[c0 + fl][1], acc[c0 + fl][2], acc[c0 + fl][3]);
     __syncthreads();
-    if (wave == 0) {  // lane holds rows 4 g4 + r of the block, column r16
-      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int w = 0; w < 8; ++w) {
-        const float4 q4 = reinterpret_cast<const float4*>(red)[w * 64 + lane];
-        t.x += q4.x; t.y += q4.y; t.z += q4.z; t.w += q4.w;
-      }
-      const int f0 = 144 * cb + 16 * fb + 4 * g4, i = f0 / g.xbar;
-      const size_t row0 = (size_t)i * g.FBT * 16 + (f0 - i * g.xbar);
-      const float tv[4] = {t.x, t.y, t.z, t.w};
+    for (int t = threadIdx.x; t < FC * 256; t += 512) {
+      const int oc = t & 15, r = (t >> 4) & 3, gq = (t >> 6) & 3, fl = t >> 8;
+      const int ln = gq * 16 + oc;
+      float sum = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gws[(row0 + r) * g.Opad + o] = tv[r];
+      for (int w = 0; w < 8; ++w) sum += red[((w * FC + fl) * 64 + ln) * 4 + r];
+      const int f0 = 144 * cb + 16 * (c0 + fl) + 4 * gq, i = f0 / g.xbar;
+      const size_t row0 = (size_t)i * g.FBT * 16 + (f0 - i * g.xbar);
+      gws[(row0 + r) * g.Opad + ob * 16 + oc] = sum;
     }
     __syncthreads();
   }

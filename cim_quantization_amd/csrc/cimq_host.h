@@ -874,8 +874,9 @@ inline PlanG5 g5_plan_compute(const Geo& g) {
   const int want = std::max(1, tune("GW5_BLOCKS", 512) / p.pairs);
   v.nst = std::max(1, (v.nmt + want - 1) / want);
   v.nchunks = (v.nmt + v.nst - 1) / v.nst;
-  // the A-ready patch (or the wave-sum buffer), then cD_kj (16 floats) and the code -> word table (260)
-  p.lds = std::max((size_t)16 * v.IPM * v.RH * v.WP * 8, (size_t)8 * 64 * 16) + 64 + 4 * 260;
+  // the A-ready patch (or the epilogue's wave-sum buffer, three 16-row blocks of 8 waves), then cD_kj (16
+  // floats) and the code -> word table (260)
+  p.lds = std::max((size_t)16 * v.IPM * v.RH * v.WP * 8, (size_t)3 * 8 * 64 * 16) + 64 + 4 * 260;
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
 }

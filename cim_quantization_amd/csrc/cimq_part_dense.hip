@@ -243,7 +243,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void d
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int c0 = i * g.xbar + ks * 64 + 16 * g4;
+#ifdef CIMQ_EXP_DENSE_NOX
+      if (true) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) w[ks][e] = (uint32_t)(mrow * 131 + c0 * 7 + e) & 0x01010101u;
+      } else if (c0 < g.C) {
+#else
       if (c0 < g.C) {
+#endif
         const uint4* src = reinterpret_cast<const uint4*>(xcf + ((size_t)mrow * g.C + c0) * 4);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -256,12 +263,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void d
       }
     }
     __syncthreads();  // the previous tile's readers of prm / wkl are done
+#ifdef CIMQ_EXP_DENSE_NOSTAGE
+    if (i == 0)
+#endif
     for (int t = threadIdx.x; t < NKJ * 64; t += 512) {
       const int col = t & 63, jk = t >> 6, j = jk / NBW, k = jk - j * NBW;
       const int pi = pidx(g, i, j, k, og * 64 + col);
       prm[t] = make_int4(pp.thi[pi], pp.tlo[pi], pp.mlo[pi], pp.mhi[pi]);
       cfl[t] = pp.coef[pi];
     }
+#ifdef CIMQ_EXP_DENSE_NOSTAGE
+    if (i == 0)
+#endif
     stage_w(i, 0);
     v4i xs[NBA][KS];
 #pragma unroll
@@ -278,7 +291,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void d
     for (int ob = 0; ob < 4; ++ob) {
       if (ob == 2) {
         __syncthreads();  // half 0 read by every wave
+#ifndef CIMQ_EXP_DENSE_NOSTAGE
         stage_w(i, 1);
+#endif
         __syncthreads();
       }
       float acc[4];
