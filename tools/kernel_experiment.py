@@ -67,6 +67,9 @@ VARIANTS = {
     "dense_noadc": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE"],  # cfg5 forward attribution (timing only)
     "dense_nostore": ["CIMQ_EXP_DENSE_NOSTORE"],
     "dense_noprm": ["CIMQ_EXP_DENSE_NOPRM"],
+    "dense_skel_nox": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE", "CIMQ_EXP_DENSE_NOX"],
+    "dense_skel_nostage": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE", "CIMQ_EXP_DENSE_NOSTAGE"],
+    "dense_skel_none": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE", "CIMQ_EXP_DENSE_NOSTAGE", "CIMQ_EXP_DENSE_NOX"],
     "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
 }
