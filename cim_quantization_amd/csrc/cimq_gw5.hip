@@ -19,6 +19,8 @@
 //     waves are summed in LDS in wave order and the block writes its part of the chunk's slab (the
 //     module epilogue sums the slabs in chunk order: deterministic).
 #pragma once
+#include <type_traits>
+
 #include "cimq_v7.hip"
 
 namespace cimq {
@@ -43,7 +45,11 @@ struct G5 {
 
 #ifdef CIMQ_TU_GW5
 // SS: the conv stride (1 or 2): a compile-time constant, so the pixel-pair offsets stay immediates
-template <int SS, bool CODES>  // CODES: G5::codes, a compile-time choice of the staging's load width
+// SP: the row blocks of the block's two tiles split at fb = 8 - (cb mod 8) (its first 144 cb mod 128 rows lie in the
+// first tile), compiled in so that the MFMA chains of consecutive row blocks are not separated by branches and
+// their A reads issue ahead: 8 when every block has cb = 0 (16 input channels), 78 for cb 0 / 1 (32 input
+// channels: two m-tile loops); 0: a uniform per-block table
+template <int SS, bool CODES, int SP>  // CODES: G5::codes, a compile-time choice of the staging's load width
 __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
                         const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
@@ -112,6 +118,9 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const float invRH = 1.f / (float)v.RH, invIPM = 1.f / (float)v.IPM;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;
   const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
+  // the m-tile loop with the block's row-block split SPL compiled in (0: the per-block table)
+  auto mtiles = [&](auto spc) __attribute__((always_inline)) {
+    constexpr int SPL = decltype(spc)::value;
   for (int mt = mt_lo; mt < mt_hi; ++mt) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) asm volatile("" : "+v"(aoffp[k]));
@@ -157,27 +166,26 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     const int n = 16 * CH * g.W;
     const int ih0 = oh0 * SS - 1;  // patch row 0 (pad 1)
     const int xb = (b0 * g.C + 16 * cb) * HWi + ih0 * g.W;  // (image b0, channel 16 cb, row ih0)
+    // (branch-free: every item loads -- out-of-patch and out-of-image items from element 0 -- and selects, so the
+    // SU reads are in flight together; a branch around each load made hipcc wait for each before the next)
     auto ld = [&](int base, uint32_t (&wv)[SU]) {
 #pragma unroll
       for (int u = 0; u < SU; ++u) {
         const int idx = base + u * 512;
-        wv[u] = CODES ? kZeroCode : 0u;
-        if (idx < n) {
-          const int col = idx & (g.W - 1), cr = idx >> v.lwi;
-          const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
-          const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
-          const int ih = ih0 + row;
-          if ((unsigned)ih < (unsigned)g.H) {
-            const int xi = xb + (slt * g.C + c) * HWi + row * g.W + col;
-            // (a code byte, expanded below through the LDS table, or the word itself)
-            // (unsigned offsets: the loads take the scalar base + 32-bit offset form)
+        const int col = idx & (g.W - 1), cr = idx >> v.lwi;
+        const int rr = sdiv5(cr, invRH), row = cr - rr * v.RH;  // rr = c * IPM + slot
+        const int c = sdiv5(rr, invIPM), slt = rr - c * v.IPM;
+        const int ih = ih0 + row;
+        const bool ok = idx < n && (unsigned)ih < (unsigned)g.H;
+        // (a code byte, expanded below through the LDS table, or the word itself)
+        // (unsigned offsets: the loads take the scalar base + 32-bit offset form)
+        const uint32_t xi = ok ? (uint32_t)(xb + (slt * g.C + c) * HWi + row * g.W + col) : 0u;
 #ifdef CIMQ_EXP_GW5_NOLOAD
-            wv[u] = CODES ? (uint32_t)(xi & 7) : (uint32_t)xi * 0x010203u;
+        const uint32_t w = CODES ? (xi & 7u) : xi * 0x010203u;
 #else
-            wv[u] = CODES ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[(uint32_t)xi] : xcb[(uint32_t)xi];
+        const uint32_t w = CODES ? (uint32_t)reinterpret_cast<const uint8_t*>(xcb)[xi] : xcb[xi];
 #endif
-          }
-        }
+        wv[u] = ok ? w : (CODES ? (uint32_t)kZeroCode : 0u);
       }
     };
     auto stv = [&](int base, uint32_t (&wv)[SU]) {
@@ -208,67 +216,83 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     }
     __syncthreads();
 
+    {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
-      const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
-      const int pin = pin0 + e0;  // within the image slot
-      const int poff = (sl * v.RH + (pin >> v.lwo) * SS) * v.WP + (pin & (Wo - 1)) * SS;
+      for (int s = 0; s < 2; ++s) {
+        const int e0 = 2 * s;  // pixels e0, e0 + 1 of this lane's four (same output row: Wo % 4 == 0)
+        const float gv0 = (&gq.x)[e0], gv1 = (&gq.x)[e0 + 1];
+        const int pin = pin0 + e0;  // within the image slot
+        const int poff = (sl * v.RH + (pin >> v.lwo) * SS) * v.WP + (pin & (Wo - 1)) * SS;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (q >= ntl) break;
-        const uint32_t s0 = sq[q][e0], s1 = sq[q][e0 + 1];
+        for (int q = 0; q < 2; ++q) {
+          if (q >= ntl) break;
+          const uint32_t s0 = sq[q][e0], s1 = sq[q][e0 + 1];
 #ifdef CIMQ_EXP_GW5_NOGA
-        if (false) {
+          if (false) {
 #else
-        if (own[q]) {
+          if (own[q]) {
 #endif
-          // grad_alpha partials (lsq.py:321-333): code * g, the code the signed 2-bit field at bit 3kj + 1
+            // grad_alpha partials (lsq.py:321-333): code * g, the code the signed 2-bit field at bit 3kj + 1
 #pragma unroll
-          for (int kj = 0; kj < 9; ++kj) {
-            const int c0 = ((int)(s0 << (29 - 3 * kj))) >> 30, c1 = ((int)(s1 << (29 - 3 * kj))) >> 30;
-            ga[q][kj] = __builtin_fmaf((float)c1, gv1, __builtin_fmaf((float)c0, gv0, ga[q][kj]));
-          }
-        }
-        // B operand: g * D_j of the two pixels, slots (j = 0, 1, 2, 0), split hi / mid / lo
-        float d[8];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          float D0, D1;
-          if (std_mask) {
-            D0 = (float)(__popc(s0 & pass_mask_j(j, 3, 3)) << j);
-            D1 = (float)(__popc(s1 & pass_mask_j(j, 3, 3)) << j);
-          } else {
-            D0 = D1 = 0.f;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              const int bit = 3 * (k * 3 + j);
-              D0 += ((s0 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
-              D1 += ((s1 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
+            for (int kj = 0; kj < 9; ++kj) {
+              const int c0 = ((int)(s0 << (29 - 3 * kj))) >> 30, c1 = ((int)(s1 << (29 - 3 * kj))) >> 30;
+              ga[q][kj] = __builtin_fmaf((float)c1, gv1, __builtin_fmaf((float)c0, gv0, ga[q][kj]));
             }
           }
-          d[j] = gv0 * D0;
-          d[4 + j] = gv1 * D1;
-        }
-        d[3] = d[7] = 0.f;
-        v8bf bh, bm, bl;
-        split3x8(d, bh, bm, bl);
+          // B operand: g * D_j of the two pixels, slots (j = 0, 1, 2, 0), split hi / mid / lo
+          float d[8];
 #pragma unroll
-        for (int fb = 0; fb < 9; ++fb) {
-          if (atl[fb] != q) continue;  // uniform: the 16-row blocks of this tile
-          const int ao = (int)((aoffp[fb >> 1] >> (16 * (fb & 1))) & 0xFFFFu);
-          const uint2 a0 = pat[ao + poff], a1 = pat[ao + poff + SS];
-          const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
+          for (int j = 0; j < 3; ++j) {
+            float D0, D1;
+            if (std_mask) {
+              D0 = (float)(__popc(s0 & pass_mask_j(j, 3, 3)) << j);
+              D1 = (float)(__popc(s1 & pass_mask_j(j, 3, 3)) << j);
+            } else {
+              D0 = D1 = 0.f;
+#pragma unroll
+              for (int k = 0; k < 3; ++k) {
+                const int bit = 3 * (k * 3 + j);
+                D0 += ((s0 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
+                D1 += ((s1 >> bit) & 1u) ? cdl[k * 3 + j] : 0.f;
+              }
+            }
+            d[j] = gv0 * D0;
+            d[4 + j] = gv1 * D1;
+          }
+          d[3] = d[7] = 0.f;
+          v8bf bh, bm, bl;
+          split3x8(d, bh, bm, bl);
+#pragma unroll
+          for (int fb = 0; fb < 9; ++fb) {
+            // the 16-row blocks of this tile: fb < SP in the block's first tile, the rest in its second (compile
+            // time: the MFMA chains of consecutive row blocks are not separated by branches, so their A reads
+            // issue ahead); SP 0: the uniform per-block table
+            if constexpr (SPL > 0) {
+              if (q == 0 ? fb >= SPL : fb < SPL) continue;
+            } else {
+              if (atl[fb] != q) continue;
+            }
+            const int ao = (int)((aoffp[fb >> 1] >> (16 * (fb & 1))) & 0xFFFFu);
+            const uint2 a0 = pat[ao + poff], a1 = pat[ao + poff + SS];
+            const v8bf a = as_v8bf(v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y});
 #ifdef CIMQ_EXP_GW5_NOMFMA
-          acc[fb][0] += (float)a[0] + (float)bh[0] + (float)bm[1] + (float)bl[2];
-          continue;
+            acc[fb][0] += (float)a[0] + (float)bh[0] + (float)bm[1] + (float)bl[2];
+            continue;
 #endif
-          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
-          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
-          acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[fb], 0, 0, 0);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm, acc[fb], 0, 0, 0);
+            acc[fb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[fb], 0, 0, 0);
+          }
         }
       }
     }
+  }
+  };
+  if constexpr (SP == 78) {  // 32 input channels: input-channel block 0 splits at 8, block 1 at 7
+    if (cb == 0) mtiles(std::integral_constant<int, 8>{});
+    else mtiles(std::integral_constant<int, 7>{});
+  } else {
+    mtiles(std::integral_constant<int, SP>{});
   }
 
   // the block's part of its chunk's slab: the 8 waves summed in LDS in wave order

@@ -12,8 +12,13 @@ int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* g
   if (W.nchunks_bwd != p.v.nchunks) return fail(CIMQ_EINVAL, "internal: cim_bwd_gw5 slab count mismatch");
   G5 v = p.v;
   v.codes = ctx_codes(g) ? 1 : 0;  // the forward wrote code bytes (cim_fwd5_kernel on the module path)
-  auto kern = g.SH == 2 ? (v.codes ? cim_bwd_gw5_kernel<2, true> : cim_bwd_gw5_kernel<2, false>)
-                        : (v.codes ? cim_bwd_gw5_kernel<1, true> : cim_bwd_gw5_kernel<1, false>);
+  // the row-block split compiled in: 16 input channels (every block in input-channel block 0) and 32 (blocks 0 / 1)
+  const int sp = !tune("GW5_SP8", 1) ? 0 : g.C == 16 ? 8 : (g.C == 32 && tune("GW5_SP78", 1)) ? 78 : 0;
+#define CIMQ_GW5_K(SS_, C_) (sp == 8 ? cim_bwd_gw5_kernel<SS_, C_, 8> : sp == 78 ? cim_bwd_gw5_kernel<SS_, C_, 78> \
+                                                                       : cim_bwd_gw5_kernel<SS_, C_, 0>)
+  auto kern = g.SH == 2 ? (v.codes ? CIMQ_GW5_K(2, true) : CIMQ_GW5_K(2, false))
+                        : (v.codes ? CIMQ_GW5_K(1, true) : CIMQ_GW5_K(1, false));
+#undef CIMQ_GW5_K
   CIMQ_TRY(set_lds(kern, p.lds));
   const int slot = prof_begin(KID_GW_V7, g, s);
   hipLaunchKernelGGL(kern, dim3(p.v.nchunks, p.pairs), dim3(512), p.lds, s, g, v,

@@ -23,6 +23,7 @@ sys.path.insert(0, REPO)
 # DESIGN.md section 4.
 VARIANTS = {
     "base": [],
+    "cur": [],  # the working tree (a copy of base built later)
     # round 4: the fused backward (cimq_fused.hip) and the first conv's (cimq_c1.hip)
     "f_nogx": ["CIMQ_EXP_F_NOGX"],
     "f_nogw": ["CIMQ_EXP_F_NOGW"],
