@@ -45,7 +45,7 @@ PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD-32 x 2.4 GHz (a wa
 OVERLAP = os.environ.get("CIMQ_BENCH_OVERLAP", "0") == "1"
 # CIMQ_BENCH_RECOMPUTE=1: the layers run with Conv2dLSQCiM.recompute_psum (CIMQ_OPT_RECOMPUTE)
 RECOMPUTE = os.environ.get("CIMQ_BENCH_RECOMPUTE", "0") == "1"
-TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r05_final", "pmc_traffic.json"))
+TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r06_final", "pmc_traffic.json"))
 # the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
 # prefixes (the keys of pmc_traffic.json); every launch of a family is timed, all its instantiations
 FAMILIES = {"fwd_v7": ("cimq::cim_fwd_v3_kernel<", "cimq::cim_fwd5_kernel"), "bwd_fused": "cimq::cim_bwd_fused_kernel<",
