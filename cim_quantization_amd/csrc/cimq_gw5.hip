@@ -117,7 +117,11 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int HWi = g.H * g.W;
   const float invRH = 1.f / (float)v.RH, invIPM = 1.f / (float)v.IPM;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;
+#ifdef CIMQ_EXP_GW5_EMPTY  // attribution builds only: the prologue and the slab epilogue without any m-tile
+  const int mt_lo = blockIdx.x * v.nst, mt_hi = mt_lo;
+#else
   const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
+#endif
   // the m-tile loop with the block's row-block split SPL compiled in (0: the per-block table)
   auto mtiles = [&](auto spc) __attribute__((always_inline)) {
     constexpr int SPL = decltype(spc)::value;

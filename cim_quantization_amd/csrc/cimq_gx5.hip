@@ -116,6 +116,9 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
     const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
     v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+#ifdef CIMQ_EXP_GX5_CHAINS
+    v4f acc1 = v4f{0.f, 0.f, 0.f, 0.f};
+#endif
     // grad_out of the m-tile's G-patch items, both output halves: read once here, used by every tile's step
     // (it was re-read per tile)
     float gvr[2][2][4];
@@ -225,12 +228,22 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const v8bf am = as_v8bf(*reinterpret_cast<const v4i*>(pa + PLANE + 64 * s));
           const v8bf al = as_v8bf(*reinterpret_cast<const v4i*>(pa + 2 * PLANE + 64 * s));
           const v8bf w = as_v8bf(wb[(p * 2 + s) * CBN * 64]);
+#ifdef CIMQ_EXP_GX5_CHAINS  // attribution builds: the two K-steps into separate accumulators (two MFMA chains)
+          v4f& a2 = s == 0 ? acc : acc1;
+          a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, a2, 0, 0, 0);
+          a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, w, a2, 0, 0, 0);
+          a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w, a2, 0, 0, 0);
+#else
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, w, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w, acc, 0, 0, 0);
+#endif
         }
       }
     }
+#ifdef CIMQ_EXP_GX5_CHAINS
+    acc += acc1;
+#endif
     // acc[r]: input pixel (r0 + rl, iw0 + 4 g4 + r), channel c_lo + r16: scale, LSQ activation backward, store
     const int ih = r0 + rl, iw = iw0 + 4 * g4;
     const int gi = ((b * g.C + c_lo + r16) * g.H + ih) * g.W + iw;
