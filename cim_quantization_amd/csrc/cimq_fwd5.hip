@@ -281,6 +281,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
         }
       };
       // (one instance of each phase: the first round, which every thread runs, holds the barrier)
+#ifdef CIMQ_EXP_FWD5_NOSTAGE  // attribution builds only: the patch staged for the block's first m-tile only
+      if (mt != (int)blockIdx.x) {
+        __syncthreads();
+        if (v.ngrp > 1) stage_b(q);
+      } else
+#endif
       for (int base = (int)threadIdx.x, first = 1; first || base < n; base += SU * NT, first = 0) {
         ldx(base);
         if (first) {
@@ -311,9 +317,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
             for (int k = 0; k < 3; ++k)
 #pragma unroll
               for (int j = 0; j < 3; ++j)
+#ifdef CIMQ_EXP_FWD5_NOMFMA  // attribution builds only (tools/kernel_experiment.py): wrong results
+                ps[k * 3 + j] = (first && s == 0) ? (a[j] ^ w[k]) : (ps[k * 3 + j] + (a[j] ^ w[k]));
+#else
                 ps[k * 3 + j] = (first && s == 0)
                                     ? __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], v4i{0, 0, 0, 0}, 0, 0, 0)
                                     : __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[k], ps[k * 3 + j], 0, 0, 0);
+#endif
           }
         };
         ksteps(v.tc0[i], true);  // f5_plan: every tile has at least one pair
@@ -332,6 +342,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const int p = ps[k * 3 + j][r];
+#ifdef CIMQ_EXP_FWD5_NOADC
+                acc[r] += (float)(p ^ pv.x) * cf;
+                continue;
+#endif
                 const uint64_t mhi = __builtin_amdgcn_ballot_w64(p >= pv.x);
                 const uint64_t mlo = __builtin_amdgcn_ballot_w64(p <= pv.y);
                 const uint64_t mps = WST ? __builtin_amdgcn_ballot_w64((unsigned)(p - pv.z) <= (unsigned)pv.w) : 0ull;

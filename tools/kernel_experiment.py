@@ -73,6 +73,10 @@ VARIANTS = {
     "dense_skel_none": ["CIMQ_EXP_DENSE_NOADC", "CIMQ_EXP_DENSE_NOSTORE", "CIMQ_EXP_DENSE_NOSTAGE", "CIMQ_EXP_DENSE_NOX"],
     "gw5_empty": ["CIMQ_EXP_GW5_EMPTY"],  # gw5's prologue + epilogue only
     "gw5_empty_noepi": ["CIMQ_EXP_GW5_EMPTY", "CIMQ_EXP_GW5_NOEPI"],
+    "fwd5_noadc": ["CIMQ_EXP_FWD5_NOADC"],  # fwd5 attribution (timing only)
+    "fwd5_nomfma": ["CIMQ_EXP_FWD5_NOMFMA"],
+    "fwd5_nostage": ["CIMQ_EXP_FWD5_NOSTAGE"],
+    "fwd5_skel": ["CIMQ_EXP_FWD5_NOADC", "CIMQ_EXP_FWD5_NOMFMA", "CIMQ_EXP_FWD5_NOSTAGE"],
     "gx5_chains": ["CIMQ_EXP_GX5_CHAINS"],  # gx5's two K-steps in separate MFMA accumulators
     "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
