@@ -182,7 +182,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512 * NOB, 512 * NOB), amd
   act_lut_build_q<3>(g, sa, sgn, alut);  // entries 0 .. Qp + 1 (NaN), then the block barrier
   // ctx codes: the table grad_w expands them with (code e -> ctx word), written once per launch
   if (WST && v.codes && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x) cal[t] = alut[2 * t + 1];
+    for (int t = threadIdx.x; t <= (int)g.lsq_qp + 1; t += blockDim.x) {
+      cal[t] = alut[2 * t + 1];
+      if (t == 0) cal[kCalFlag] = kCodesMagic;  // the ctx holds code bytes (checked by grad_w)
+    }
 
   // this lane's A-operand pixel (image slot, output row / col) and its three position offsets
   const int Wo = 1 << v.lwo;

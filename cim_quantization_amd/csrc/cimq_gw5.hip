@@ -76,6 +76,8 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       *reinterpret_cast<uint32_t*>(smem + alut_off + 4 * t) = cal[t];
     if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + alut_off + 4 * kZeroCode) = 0u;
   }
+  // the ctx format the forward wrote (kCalFlag): code bytes expected; a mismatch poisons the outputs
+  const bool fmt_ok = !CODES || cal[kCalFlag] == kCodesMagic;
   // padding columns 0 and WP-1: zero once
   for (int t = threadIdx.x; t < 16 * CH * 2; t += blockDim.x) {
     const int side = t & 1, cr = t >> 1;
@@ -337,7 +339,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       for (int w = 0; w < 8; ++w) sum += red[((w * FC + fl) * 64 + ln) * 4 + r];
       const int f0 = 144 * cb + 16 * (c0 + fl) + 4 * gq, i = f0 / g.xbar;
       const size_t row0 = (size_t)i * g.FBT * 16 + (f0 - i * g.xbar);
-      gws[(row0 + r) * g.Opad + ob * 16 + oc] = sum;
+      gws[(row0 + r) * g.Opad + ob * 16 + oc] = fmt_ok ? sum : __builtin_nanf("");
     }
     __syncthreads();
   }
@@ -358,7 +360,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
       const int kj = threadIdx.x >> 4, oc = threadIdx.x & 15;
       float t = 0.f;
       for (int w = 0; w < 8; ++w) t += red[(w * 9 + kj) * 16 + oc];
-      gas[((size_t)(i_lo + q) * 9 + kj) * g.Opad + ob * 16 + oc] = t;
+      gas[((size_t)(i_lo + q) * 9 + kj) * g.Opad + ob * 16 + oc] = fmt_ok ? t : __builtin_nanf("");
     }
     __syncthreads();
   }

@@ -219,7 +219,7 @@ inline CtxLayout ctx_layout_compute(const Geo& g) {
   L.wbytes = o;
   L.xcode = o; o = align256(o + (size_t)g.Nin * g.NBP);  // forward slice bytes
   L.xhat = o; o = align256(o + (size_t)g.Nin * g.NBP);   // backward (int8 ctx) slice bytes
-  L.alut = o; o = align256(o + (size_t)4 * 260);         // ctx codes: code -> ctx word (ctx_codes)
+  L.alut = o; o = align256(o + (size_t)4 * 301);         // ctx codes: code -> ctx word (ctx_codes), format word 300
   // per-partial-sum state words written by the fast forward (cimq_kernels_v3.hip: StWord)
   // (v7: one uint32 per (i, m, o) -- never larger for nbw >= 2; the max covers nbw == 1)
   // state words: per-(k) words of the v3-v6 kernels, or the v7 compact words (4 B, or three

@@ -334,6 +334,14 @@ __device__ inline uint32_t st_bits(bool pass, float code) {
 
 // shift a bit in: x * 2 + c in one v_addc_co_u32 whose carry-in is the compare's lane mask
 // (the compiler spends a cndmask + shift/or on the plain expression)
+// The ctx's code -> word table region (CtxLayout::alut, 1,280 bytes) also carries a format word at entry
+// kCalFlag: cim_fwd5_kernel writes kCodesMagic there when it stores one activation code byte per ctx element
+// (ctx_codes), and cim_bwd_gw5_kernel's code-byte instance checks it -- a ctx written in the other format
+// (a forward / backward planned differently, e.g. a tuning knob changed in between) yields NaN grad_w and
+// grad_alpha partials instead of silently reading words as codes.
+constexpr int kCalFlag = 300;
+constexpr uint32_t kCodesMagic = 0xC0DE5EEDu;
+
 __device__ inline uint32_t shin(uint32_t x, uint64_t m) {
   uint32_t r;
   uint64_t co;
