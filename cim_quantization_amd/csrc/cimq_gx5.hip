@@ -150,7 +150,11 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
 #pragma unroll
       for (int u = 0; u < NWI; ++u) {
         const int idx = threadIdx.x + u * 512;
+#ifdef CIMQ_EXP_GX5_NOLOAD  // attribution builds only: no global reads in the step (wrong results)
+        if (idx < NW5) wv[u] = v4i{idx, ih2, u, 1};
+#else
         if (idx < NW5) wv[u] = wg5[ih2 * NW5 + idx];
+#endif
       }
       uint4 s4r[2];
 #pragma unroll
@@ -161,7 +165,11 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
         s4r[kk] = make_uint4(0u, 0u, 0u, 0u);
         if (it < NG && (unsigned)oh < (unsigned)g.Ho) {
           const int m = b * g.P + oh * g.Wo + col;
+#ifdef CIMQ_EXP_GX5_NOLOAD
+          s4r[kk] = make_uint4((uint32_t)m, (uint32_t)it, 7u, (uint32_t)i);
+#else
           s4r[kk] = *reinterpret_cast<const uint4*>(st + ((i * g.M + m) * g.O + 4 * ((it & 3) + 4 * h)));
+#endif
         }
       }
       __syncthreads();  // the previous step's (or m-tile's) MFMAs are done with the patch and weights
@@ -210,13 +218,59 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           }
         }
       };
+#ifndef CIMQ_EXP_GX5_NOBUILD  // attribution builds only: the G patch left as the first step built it
       if (std_mask) build(std::true_type{});
       else build(std::false_type{});
+#else
+      if (mt == (int)blockIdx.x && i == 0) {
+        if (std_mask) build(std::true_type{});
+        else build(std::false_type{});
+      }
+#endif
       __syncthreads();
       // the wave's 16 input pixels x 16 channels: 9 positions x 2 K-steps x 3 planes, unless tile i holds
       // none of the block's rows (f = 9 c + p for c in c_lo .. c_hi)
       if (9 * c_hi + 8 < i * g.xbar || 9 * c_lo >= (i + 1) * g.xbar) continue;
       const v4i* wb = reinterpret_cast<const v4i*>(smem + OW5) + cb * 64 + lane;
+#ifdef CIMQ_EXP_GX5_DPP
+      // (tried, round 6: 5 us per launch SLOWER than the nine reads below) per kernel row kh the wave reads only
+      // the kw = 1 window; kw = 0 / 2 are its pixels shifted by one lane within each 16-lane row (DPP row_shl /
+      // row_shr: the pixels of a row are consecutive columns), the row's edge lane (r16 = 15 for kw = 0, r16 = 0
+      // for kw = 2) reading its one column outside the window by itself
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const uint8_t* pc = smem + (size_t)((rl + 2 - kh) * WP + iw0 + r16 + 1) * 96 + 16 * g4;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          v4i c[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) c[pl] = *reinterpret_cast<const v4i*>(pc + pl * PLANE + 64 * s);
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int p = kh * 3 + kw;
+            const v8bf w = as_v8bf(wb[(p * 2 + s) * CBN * 64]);
+            v4i a[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+              if (kw == 1) {
+                a[pl] = c[pl];
+              } else {
+                // kw = 0: lane r16 takes pixel r16 + 1 (row_shl:1); kw = 2: pixel r16 - 1 (row_shr:1)
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                  a[pl][d] = kw == 0 ? __builtin_amdgcn_update_dpp(0, c[pl][d], 0x101, 0xF, 0xF, true)
+                                     : __builtin_amdgcn_update_dpp(0, c[pl][d], 0x111, 0xF, 0xF, true);
+                if (r16 == (kw == 0 ? 15 : 0))
+                  a[pl] = *reinterpret_cast<const v4i*>(pc + (kw == 0 ? 96 : -96) + pl * PLANE + 64 * s);
+              }
+            }
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_v8bf(a[0]), w, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_v8bf(a[1]), w, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_v8bf(a[2]), w, acc, 0, 0, 0);
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int p = 0; p < 9; ++p) {
         const int kh = p / 3, kw = p - 3 * kh;
@@ -228,6 +282,10 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
           const v8bf am = as_v8bf(*reinterpret_cast<const v4i*>(pa + PLANE + 64 * s));
           const v8bf al = as_v8bf(*reinterpret_cast<const v4i*>(pa + 2 * PLANE + 64 * s));
           const v8bf w = as_v8bf(wb[(p * 2 + s) * CBN * 64]);
+#ifdef CIMQ_EXP_GX5_NOMFMA
+          acc[0] += (float)ah[0] + (float)am[1] + (float)al[2] + (float)w[3];
+          continue;
+#endif
 #ifdef CIMQ_EXP_GX5_CHAINS  // attribution builds: the two K-steps into separate accumulators (two MFMA chains)
           v4f& a2 = s == 0 ? acc : acc1;
           a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w, a2, 0, 0, 0);
@@ -240,6 +298,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
 #endif
         }
       }
+#endif
     }
 #ifdef CIMQ_EXP_GX5_CHAINS
     acc += acc1;

@@ -77,6 +77,11 @@ VARIANTS = {
     "fwd5_nomfma": ["CIMQ_EXP_FWD5_NOMFMA"],
     "fwd5_nostage": ["CIMQ_EXP_FWD5_NOSTAGE"],
     "fwd5_skel": ["CIMQ_EXP_FWD5_NOADC", "CIMQ_EXP_FWD5_NOMFMA", "CIMQ_EXP_FWD5_NOSTAGE"],
+    "gx5_nobuild": ["CIMQ_EXP_GX5_NOBUILD"],  # gx5 attribution (timing only)
+    "gx5_nomfma": ["CIMQ_EXP_GX5_NOMFMA"],
+    "gx5_noload": ["CIMQ_EXP_GX5_NOLOAD"],
+    "gx5_skel": ["CIMQ_EXP_GX5_NOBUILD", "CIMQ_EXP_GX5_NOMFMA", "CIMQ_EXP_GX5_NOLOAD"],
+    "gx5_dpp": ["CIMQ_EXP_GX5_DPP"],  # gx5's kw shifts by DPP instead of nine A reads per K-step (slower)
     "gx5_chains": ["CIMQ_EXP_GX5_CHAINS"],  # gx5's two K-steps in separate MFMA accumulators
     "r6_nopf": ["CIMQ_EXP_R6_NO_WFPF", "CIMQ_EXP_R6_NO_XFPF"],  # without the weight-fragment / x prefetches
     "r6_skel": ["CIMQ_EXP_R6_NOA", "CIMQ_EXP_R6_NOG", "CIMQ_EXP_R6_NOGW", "CIMQ_EXP_R6_NOGX", "CIMQ_EXP_R6_NOFIN"],
