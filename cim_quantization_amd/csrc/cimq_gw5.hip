@@ -43,17 +43,19 @@ struct G5 {
   int nchunks; // blocks = slab chunks
 };
 
-#ifdef CIMQ_TU_GW5
+#if defined(CIMQ_TU_GW5) || defined(CIMQ_TU_GXW5)
 // SS: the conv stride (1 or 2): a compile-time constant, so the pixel-pair offsets stay immediates
 // SP: the row blocks of the block's two tiles split at fb = 8 - (cb mod 8) (its first 144 cb mod 128 rows lie in the
 // first tile), compiled in so that the MFMA chains of consecutive row blocks are not separated by branches and
 // their A reads issue ahead: 8 when every block has cb = 0 (16 input channels), 78 for cb 0 / 1 (32 input
 // channels: two m-tile loops); 0: a uniform per-block table
 template <int SS, bool CODES, int SP>  // CODES: G5::codes, a compile-time choice of the staging's load width
-__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
-void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
-                        const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
-                        float* __restrict__ ga_slab) {
+// the kernel body for workgroup (bx, by) (cim_bwd_gw5_kernel, and the second part of the grid of
+// cim_bwd_gxw5_kernel, behind grad_x's workgroups)
+__device__ __forceinline__ void gw5_body(int bx, int by, const Geo& g, const G5& v, const uint32_t* __restrict__ st,
+                                         const uint32_t* __restrict__ xcb, const Params& pp,
+                                         const float* __restrict__ gout, const uint32_t* __restrict__ cal,
+                                         float* __restrict__ gw_slab, float* __restrict__ ga_slab) {
   // block = (pixel chunk, input-channel block cb, output block ob): the 9 16-row blocks of rows
   // f = 144 cb .. 144 cb + 143 (the 16 channels of cb at every (kh, kw)), which touch at most two tiles
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -64,7 +66,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const int alut_off = 16 * CH * v.WP * 8 + 16 * 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int cb = blockIdx.y / g.OB16, ob = blockIdx.y - cb * g.OB16;
+  const int cb = by / g.OB16, ob = by - cb * g.OB16;
   const int o = ob * 16 + r16;
   const int i_lo = (144 * cb) / 128, i_hi = (144 * cb + 143) / 128;  // tiles of the block's rows (xbar 128)
   const int ntl = i_hi - i_lo + 1;
@@ -120,9 +122,9 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   const float invRH = 1.f / (float)v.RH, invIPM = 1.f / (float)v.IPM;
   const int tpi = g.P >= 128 ? g.P / 128 : 1;
 #ifdef CIMQ_EXP_GW5_EMPTY  // attribution builds only: the prologue and the slab epilogue without any m-tile
-  const int mt_lo = blockIdx.x * v.nst, mt_hi = mt_lo;
+  const int mt_lo = bx * v.nst, mt_hi = mt_lo;
 #else
-  const int mt_lo = blockIdx.x * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
+  const int mt_lo = bx * v.nst, mt_hi = min(mt_lo + v.nst, v.nmt);
 #endif
   // the m-tile loop with the block's row-block split SPL compiled in (0: the per-block table)
   auto mtiles = [&](auto spc) __attribute__((always_inline)) {
@@ -304,7 +306,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   // the block's part of its chunk's slab: the 8 waves summed in LDS in wave order
 #ifdef CIMQ_EXP_GW5_NOEPI
   {
-    float* gws = gw_slab + (size_t)blockIdx.x * g.T * g.FBT * 16 * g.Opad;
+    float* gws = gw_slab + (size_t)bx * g.T * g.FBT * 16 * g.Opad;
     float t = 0.f;
 #pragma unroll
     for (int fb = 0; fb < 9; ++fb) t += acc[fb][0] + acc[fb][1] + acc[fb][2] + acc[fb][3];
@@ -319,7 +321,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);  // [8 waves][FC row blocks][64 lanes][4] (g5_plan: >= 24 KB)
   const size_t rows = (size_t)g.T * g.FBT * 16;
-  float* gws = gw_slab + (size_t)blockIdx.x * rows * g.Opad;
+  float* gws = gw_slab + (size_t)bx * rows * g.Opad;
   // three 16-row blocks at a time: every wave stores its accumulators, then all 512 threads sum the 8 waves
   // (in wave order, from 0: the sums of the one-wave reduction before, bit for bit) and store 16 consecutive
   // channels per 16 threads
@@ -344,7 +346,7 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     __syncthreads();
   }
   // grad_alpha of the owned tiles: the four lane groups, then the 8 waves
-  float* gas = ga_slab + (size_t)blockIdx.x * g.T * 9 * g.Opad;
+  float* gas = ga_slab + (size_t)bx * g.T * 9 * g.Opad;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (!own[q]) continue;  // uniform
@@ -364,6 +366,16 @@ void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint
     }
     __syncthreads();
   }
+}
+#endif  // CIMQ_TU_GW5 || CIMQ_TU_GXW5
+
+#ifdef CIMQ_TU_GW5
+template <int SS, bool CODES, int SP>
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+void cim_bwd_gw5_kernel(Geo g, G5 v, const uint32_t* __restrict__ st, const uint32_t* __restrict__ xcb, Params pp,
+                        const float* __restrict__ gout, const uint32_t* __restrict__ cal, float* __restrict__ gw_slab,
+                        float* __restrict__ ga_slab) {
+  gw5_body<SS, CODES, SP>((int)blockIdx.x, (int)blockIdx.y, g, v, st, xcb, pp, gout, cal, gw_slab, ga_slab);
 }
 #endif  // CIMQ_TU_GW5
 

@@ -69,13 +69,17 @@ __global__ void prep_wg5_kernel(Geo g, const float* __restrict__ w_q, const floa
   const WSrc ws{w_q, *sw_p, 0, 0.f, 0.f};
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) wg5_item(g, ws, wg5, t);
 }
+#endif  // CIMQ_TU_GX5
 
+#if defined(CIMQ_TU_GX5) || defined(CIMQ_TU_GXW5)
+// the kernel body for workgroup bid of nblk (cim_bwd_gx5_kernel, and the first part of the grid of
+// cim_bwd_gxw5_kernel, which runs grad_w's workgroups behind it in the same launch)
 template <int CBN>  // 16-channel input blocks = output halves (X5::CBN)
-__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 8)))
-void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i* __restrict__ wg5, Params pp,
-                        const float* __restrict__ sw_p, const float* __restrict__ sa_p,
-                        const float* __restrict__ gout, const float* __restrict__ x, float* __restrict__ gx,
-                        float* __restrict__ gsa_part) {
+__device__ __forceinline__ void gx5_body(int bid, int nblk, const Geo& g, const X5& v, const uint32_t* __restrict__ st,
+                                         const v4i* __restrict__ wg5, const Params& pp, const float* __restrict__ sw_p,
+                                         const float* __restrict__ sa_p, const float* __restrict__ gout,
+                                         const float* __restrict__ x, float* __restrict__ gx,
+                                         float* __restrict__ gsa_part) {
   // LDS: G patch, three planes [6 rows][W + 2 cols][48 (k, o)] bf16 (96 B per pixel; 32 B of slack after
   // the last plane: the padded K-step reads past a pixel's 48 values), then the tile's weight operand
   // [9 p][2 s][64 lanes] (16 B each), then the mask coefficients and the partials
@@ -113,7 +117,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   const int gstride = g.onchw ? g.P : 1;  // grad_out element stride between output channels
 
   const int NG = 6 * g.W * 4;  // G patch items (row, col, 4 channels): <= 2 per thread (x5_plan)
-  for (int mt = blockIdx.x; mt < v.nmt; mt += gridDim.x) {
+  for (int mt = bid; mt < v.nmt; mt += nblk) {
     const int b = mt / v.tpi, r0 = (mt - b * v.tpi) * 4;  // input rows r0 .. r0 + 3
     v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #ifdef CIMQ_EXP_GX5_CHAINS
@@ -222,7 +226,7 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
       if (std_mask) build(std::true_type{});
       else build(std::false_type{});
 #else
-      if (mt == (int)blockIdx.x && i == 0) {
+      if (mt == bid && i == 0) {
         if (std_mask) build(std::true_type{});
         else build(std::false_type{});
       }
@@ -333,8 +337,19 @@ void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i*
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int w = 0; w < 8; ++w) t += red[w];
-    gsa_part[blockIdx.x] = t;
+    gsa_part[bid] = t;
   }
+}
+#endif  // CIMQ_TU_GX5 || CIMQ_TU_GXW5
+
+#ifdef CIMQ_TU_GX5
+template <int CBN>
+__global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 8)))
+void cim_bwd_gx5_kernel(Geo g, X5 v, const uint32_t* __restrict__ st, const v4i* __restrict__ wg5, Params pp,
+                        const float* __restrict__ sw_p, const float* __restrict__ sa_p,
+                        const float* __restrict__ gout, const float* __restrict__ x, float* __restrict__ gx,
+                        float* __restrict__ gsa_part) {
+  gx5_body<CBN>((int)blockIdx.x, (int)gridDim.x, g, v, st, wg5, pp, sw_p, sa_p, gout, x, gx, gsa_part);
 }
 #endif  // CIMQ_TU_GX5
 

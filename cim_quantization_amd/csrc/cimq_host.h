@@ -1133,6 +1133,9 @@ int launch_gx5(const Geo& g, const PlanX5& p, const uint8_t* ctx, const float* s
 int launch_prep_wg5(const Geo& g, const float* w_q, const float* sw, uint8_t* ctx, hipStream_t s);
 // cimq_part_gw5.hip: grad_w + grad_alpha slabs of the w3a3 stride-1 16 / 32-channel layers (g5_plan)
 int launch_gw5(const Geo& g, const PlanG5& p, const uint8_t* ctx, const float* gout, uint8_t* ws, hipStream_t s);
+// cimq_part_gxw5.hip: both in one launch (grad_x's workgroups, then grad_w's)
+int launch_gxw5(const Geo& g, const PlanX5& px, const PlanG5& pw, const uint8_t* ctx, const float* sw, const float* sa,
+                const float* gout, const float* x, float* gx, uint8_t* ws, hipStream_t s);
 // cimq_part_dense.hip: the dense path (dense_plan) -- forward, and grad_x + grad_w / grad_alpha slabs
 int launch_dense_fwd(const Geo& g, uint8_t* ctx, const float* sw, const float* sa, float* out, hipStream_t s);
 // shift ADC on the fast path (cimq_part_shift.hip): grad_alpha / grad_beta from the forward's state words

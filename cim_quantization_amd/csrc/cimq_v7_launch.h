@@ -17,6 +17,10 @@ int launch_v7_nb(const Geo& g, const Plan7& p, const uint8_t* ctx, const float* 
   Params pp = params_of(g, const_cast<uint8_t*>(ctx));
   const uint32_t* st = reinterpret_cast<const uint32_t*>(ctx + L.st);
   const PlanX5 px5 = x5_plan(g);
+  if ((parts & 3) == 3 && px5.ok && lsq && g.SH == 1 && tune("GXW5", 1)) {
+    const PlanG5 pg5 = g5_plan(g);
+    if (pg5.ok) return launch_gxw5(g, px5, pg5, ctx, sw, sa, gout, x, gx, ws, s);  // both kernels, one grid
+  }
   if ((parts & 1) && px5.ok && lsq) {
     CIMQ_TRY(launch_gx5(g, px5, ctx, sw, sa, gout, x, gx, ws, s));
   } else if (parts & 1) {
