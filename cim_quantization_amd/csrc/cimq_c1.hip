@@ -199,9 +199,15 @@ __global__ __launch_bounds__(512) void cim_bwd_c1_kernel(Geo g, VC1 v, const uin
     v4f acc[3];
 #pragma unroll
     for (int cb = 0; cb < 3; ++cb) acc[cb] = v4f{0.f, 0.f, 0.f, 0.f};
-    // k is a rolled loop: at most eight partial-sum MFMAs in flight (a full unroll hoists all 64 and spills)
-#pragma unroll 1
-    for (int k = 0; k < NB; ++k) {
+    using F = std::false_type;
+    using T = std::true_type;
+    // one weight slice k: its live pairs' partial sums, pass counts, codes, then grad_x's K-step.  kv is k:
+    // a compile-time constant on the standard-mask path (STD), whose pair selection j + k < 7 then folds
+    // away -- no uniform branches between the slice's MFMAs and their VALU, so the scheduler can put the
+    // partial sums of all its pairs in flight ahead of the compares; a runtime int otherwise
+    auto kiter = [&](auto kv, auto stdc) {
+      constexpr bool STD = decltype(stdc)::value;
+      const int k = kv;
       const v4i wkk = wkl[k * WAVE + lane];
       const unsigned lk = (unsigned)(live >> (8 * k)) & 0xFFu;
       int E[4] = {0, 0, 0, 0};  // as D: a count (standard mask) or float bits
@@ -254,8 +260,6 @@ __global__ __launch_bounds__(512) void cim_bwd_c1_kernel(Geo g, VC1 v, const uin
         }
         qs[j] = q;
       };
-      using F = std::false_type;
-      using T = std::true_type;
       // the live pairs (uniform branches): mask != 0; under the standard mask j + k < 7 (coefficient
       // +2^k / +2^j) and then the one pair j + k = 7 (-2^k / -2^j)
       auto pairs = [&](auto lit, auto sm) {
@@ -290,9 +294,13 @@ __global__ __launch_bounds__(512) void cim_bwd_c1_kernel(Geo g, VC1 v, const uin
           negp(std::integral_constant<int, 7>{});
         }
       };
-      if (literal) pairs(std::true_type{}, std::false_type{});
-      else if (stdm) pairs(std::false_type{}, std::true_type{});
-      else pairs(std::false_type{}, std::false_type{});
+      if constexpr (STD) {
+        pairs(F{}, T{});
+      } else {
+        if (literal) pairs(T{}, F{});
+        else if (stdm) pairs(F{}, T{});
+        else pairs(F{}, F{});
+      }
 #endif
       // grad_alpha partials of slice k's pairs, channel r16, this wave's 16 pixels: the four 16-lane
       // rows summed by two half-wave swaps (no LDS), then lane row g4 adds pairs j = g4 and g4 + 4 to
@@ -336,6 +344,30 @@ __global__ __launch_bounds__(512) void cim_bwd_c1_kernel(Geo g, VC1 v, const uin
           acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, Gl, acc[cb], 0, 0, 0);
         }
       }
+    };
+    if (stdm && !literal) {
+      // the slices unrolled, a scheduling fence after each: the pairs of one slice in flight together (a
+      // free schedule over all 36 pairs would hoist every partial sum and spill)
+      using std::integral_constant;
+      kiter(integral_constant<int, 0>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 1>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 2>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 3>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 4>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 5>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 6>{}, T{});
+      __builtin_amdgcn_sched_barrier(0);
+      kiter(integral_constant<int, 7>{}, T{});
+    } else {
+      // any other mask or the literal ADC (rare): k rolled
+#pragma unroll 1
+      for (int k = 0; k < NB; ++k) kiter(k, F{});
     }
     // ---- grad_w: B = g * D_j (lane: channel r16, pixels 4 g4 + r), A = xhat_j rows f, 16x16x16 bf16 ----
     {

@@ -314,4 +314,14 @@ __device__ inline void split3(float a, uint16_t& hi, uint16_t& mid, uint16_t& lo
 __device__ inline v8bf as_v8bf(v4i x) { return __builtin_bit_cast(v8bf, x); }
 __device__ inline v4i as_v4i(v8bf x) { return __builtin_bit_cast(v4i, x); }
 
+// (v_l + v_{l^16}) + (v_{l^32} + v_{l^48}) in every lane: the sum over the four 16-lane rows of a wave,
+// in __shfl_xor(16)-then-(32)'s order and rounding (each add is commutative, so bit-identical to it), on
+// the gfx950 row-swap permutes (VALU) instead of two LDS-crossbar ds_bpermute round trips
+__device__ inline float rows4_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float h = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
+
 }  // namespace cimq

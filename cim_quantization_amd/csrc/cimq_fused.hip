@@ -24,6 +24,8 @@
 // is one step); the slabs [image][tile][row][o] are summed in a fixed order by the module tail /
 // reduce kernels: bit-identical run to run, no atomics.
 #pragma once
+#include <type_traits>
+
 #include "cimq_v7.hip"
 
 namespace cimq {
@@ -226,6 +228,10 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
     }
     __syncthreads();  // the unit is in LDS
 
+    // the unit's two roles, compiled once per mask kind (SMC: the standard binary mask, E_k / D_j as
+    // pass-bit popcounts) so no per-element uniform branch separates their VALU and MFMA work
+    auto unit_roles = [&](auto smc) {
+      constexpr bool SMC = decltype(smc)::value;
     if (gxw) {
 #ifndef CIMQ_EXP_F_NOGX
       // ================= grad_x: G from the state words, MFMA against wcy, ring =================
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
             const int k = kb / OBX, ob = kb - k * OBX;
             const uint32_t sv = r == 0 ? sq[ob].x : r == 1 ? sq[ob].y : r == 2 ? sq[ob].z : sq[ob].w;
             float E;
-            if (std_mask) {
+            if constexpr (SMC) {
               E = ldexpf((float)__popc(sv & pass_mask_k(k, NB)), g.bsw * k);
             } else {
               E = 0.f;
@@ -270,15 +276,31 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       v4i anx[NKS];
 #pragma unroll
       for (int sk = 0; sk < NKS; ++sk) anx[sk] = wt[sk * 64];
+#ifdef CIMQ_EXP_F_PF2  // experiment: the weight blocks two (c, kh)-blocks ahead
+      v4i anx2[NKS];
+      if (ncb > 1) {
+#pragma unroll
+        for (int sk = 0; sk < NKS; ++sk) anx2[sk] = wt[(NKS + sk) * 64];
+      }
+#endif
 #pragma unroll 1
       for (int cb = 0; cb < ncb; ++cb) {
         v4i acur[NKS];
 #pragma unroll
         for (int sk = 0; sk < NKS; ++sk) acur[sk] = anx[sk];
+#ifdef CIMQ_EXP_F_PF2
+#pragma unroll
+        for (int sk = 0; sk < NKS; ++sk) anx[sk] = anx2[sk];
+        if (cb + 2 < ncb) {
+#pragma unroll
+          for (int sk = 0; sk < NKS; ++sk) anx2[sk] = wt[((cb + 2) * NKS + sk) * 64];
+        }
+#else
         if (cb + 1 < ncb) {
 #pragma unroll
           for (int sk = 0; sk < NKS; ++sk) anx[sk] = wt[((cb + 1) * NKS + sk) * 64];
         }
+#endif
         v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int sk = 0; sk < NKS; ++sk) {
@@ -353,8 +375,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
               const int code = ((int)(sv[e] << (29 - 3 * kj))) >> 30;
               q = __builtin_fmaf((float)code, gv[e], q);
             }
-            q += __shfl_xor(q, 16);
-            q += __shfl_xor(q, 32);
+            q = rows4_sum(q);
             if (g4 == 0) gal[((gwi * g.T + i) * NKJ + kj) * 16 + r16] += q;
           }
         }
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float D;
-            if (std_mask) {
+            if constexpr (SMC) {
               D = ldexpf((float)__popc(sv[e] & pass_mask_j(j, NB, NB)), g.bsa * j);
             } else {
               D = 0.f;
@@ -376,19 +397,26 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           }
           split3x8(d, bh[j], bm[j], bq[j]);
         }
+        // the row groups' MFMA chains; where the tile has all of this wave's groups (every tile but a short
+        // last one) without the per-group uniform branch, so the chains' A reads and MFMAs interleave
+        auto gw_chains = [&](auto fc) {
+          constexpr bool FULL = decltype(fc)::value;
 #pragma unroll
-        for (int n = 0; n < NGW; ++n) {
-          if (wpart + RGS * n >= ngt) continue;  // uniform
-          const int ofs = gofs[n] >= 0 ? gofs[n] + q0 : zoff;
+          for (int n = 0; n < NGW; ++n) {
+            if (!FULL && wpart + RGS * n >= ngt) continue;  // uniform
+            const int ofs = gofs[n] >= 0 ? gofs[n] + q0 : zoff;
 #pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            const __bf16* src = pl + (size_t)j * 3 * v.KWP + ofs;
-            const v8bf a = as_v8bf(*reinterpret_cast<const v4i*>(src));
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[n], 0, 0, 0);
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[n], 0, 0, 0);
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[n], 0, 0, 0);
+            for (int j = 0; j < NB; ++j) {
+              const __bf16* src = pl + (size_t)j * 3 * v.KWP + ofs;
+              const v8bf a = as_v8bf(*reinterpret_cast<const v4i*>(src));
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[j], acc[n], 0, 0, 0);
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[n], 0, 0, 0);
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j], acc[n], 0, 0, 0);
+            }
           }
-        }
+        };
+        if (wpart + RGS * (NGW - 1) < ngt) gw_chains(std::true_type{});
+        else gw_chains(std::false_type{});
       }
       // accumulator rows 16 gr + 4 g4 + r, column o: owned by this wave alone
 #pragma unroll
@@ -407,6 +435,9 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       }
 #endif
     }
+    };
+    if (std_mask) unit_roles(std::true_type{});
+    else unit_roles(std::false_type{});
 
     if (i == g.T - 1) {
       // ---- end of step: fold the input rows whose three output rows are done (lsq.py:382) ----
@@ -415,7 +446,24 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
       const int f0 = done + 1, f1 = upto;
       if (f1 >= f0) {
         const int nf = (f1 - f0 + 1) * g.C * W;
-        for (int t = threadIdx.x; t < nf; t += blockDim.x) {
+        // XB elements per thread and round, their x loads issued together ahead of the sums
+        auto fidx = [&](int t) {
+          const int iw = t & (W - 1), rest = t >> v.lw;
+          const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
+          const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
+          return (((size_t)b * g.C + c) * g.H + ih) * W + iw;
+        };
+        for (int t0 = threadIdx.x; t0 < nf; t0 += CIMQ_FOLD_XB * blockDim.x) {
+        float xb[CIMQ_FOLD_XB];
+#pragma unroll
+        for (int u = 0; u < CIMQ_FOLD_XB; ++u) {
+          const int t = t0 + u * (int)blockDim.x;
+          xb[u] = (LSQ && t < nf) ? x[fidx(t)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < CIMQ_FOLD_XB; ++u) {
+          const int t = t0 + u * (int)blockDim.x;
+          if (t >= nf) break;
           const int iw = t & (W - 1), rest = t >> v.lw;
           const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
           const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
@@ -435,7 +483,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           const float gqv = a * scale;
           if (LSQ) {
             // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v8_kernel
-            const float xv = x[gi];
+            const float xv = xb[u];
             const float y1 = xv / sa;
             const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
             const float rr2 = rintf(clv);
@@ -448,6 +496,7 @@ __global__ __launch_bounds__(512) void cim_bwd_fused_kernel(Geo g, V9 v, const u
           } else {
             gx[gi] = gqv;
           }
+        }
         }
         done = f1;
       }

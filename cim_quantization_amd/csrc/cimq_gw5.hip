@@ -353,8 +353,7 @@ __device__ __forceinline__ void gw5_body(int bx, int by, const Geo& g, const G5&
 #pragma unroll
     for (int kj = 0; kj < 9; ++kj) {
       float t = ga[q][kj];
-      t += __shfl_xor(t, 16);
-      t += __shfl_xor(t, 32);
+      t = rows4_sum(t);
       if (g4 == 0) red[(wave * 9 + kj) * 16 + r16] = t;
     }
     __syncthreads();

@@ -1111,11 +1111,9 @@ __global__ __launch_bounds__(256) void cim_bwd_gw_kernel(Geo g, const int8_t* __
                 }
               }
               // lanes l, l^16, l^32, l^48 share the column: fold the 16 pixel rows, then LDS
-              qs += __shfl_xor(qs, 16);
-              qs += __shfl_xor(qs, 32);
+              qs = rows4_sum(qs);
               if (shift) {
-                qb += __shfl_xor(qb, 16);
-                qb += __shfl_xor(qb, 32);
+                qb = rows4_sum(qb);
               }
               if (g4 == 0 && (INIT || has_code)) {
                 qacc[(wave * nkj + kj) * ncol + ocol] += qs;

@@ -675,8 +675,7 @@ __global__ __launch_bounds__(512) void dense_gw_kernel(Geo g, int rows_per_chunk
 #pragma unroll
   for (int kj = 0; kj < NKJ; ++kj) {
     float q = qa[kj];
-    q += __shfl_xor(q, 16);
-    q += __shfl_xor(q, 32);
+    q = rows4_sum(q);
     if (g4 == 0) ga_slab[(((size_t)chunk * g.T + i) * NKJ + kj) * g.Opad + oo] = q;
   }
 }

@@ -144,10 +144,8 @@ __global__ __launch_bounds__(256) void shift_stats_kernel(Geo g, V3 v, const uin
 #pragma unroll
   for (int kj = 0; kj < NKJ; ++kj) {
     float a = qs[kj], c = cs[kj];
-    a += __shfl_xor(a, 16);
-    a += __shfl_xor(a, 32);
-    c += __shfl_xor(c, 16);
-    c += __shfl_xor(c, 32);
+    a = rows4_sum(a);
+    c = rows4_sum(c);
     if (g4 == 0) {
       red[(wave * 2 * NKJ + kj) * 16 + r16] = a;
       red[(wave * 2 * NKJ + NKJ + kj) * 16 + r16] = c;

@@ -561,8 +561,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_pe
 #pragma unroll
     for (int kj = 0; kj < 9; ++kj) {
       float t = ga[i][kj];
-      t += __shfl_xor(t, 16);
-      t += __shfl_xor(t, 32);
+      t = rows4_sum(t);
       if (g4 == 0) gar[((wave * T + i) * 9 + kj) * 16 + r16] = t;
     }
   __syncthreads();

@@ -31,6 +31,10 @@
 #include "cimq_kernels_v3.hip"
 #include "cimq_lsq_dev.h"
 
+#ifndef CIMQ_FOLD_XB
+#define CIMQ_FOLD_XB 1  // the grad_x folds' elements per thread and round (cimq_v7 / cimq_fused)
+#endif
+
 namespace cimq {
 
 struct V7 {
@@ -330,7 +334,24 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
     const int f0 = max(done + 1, r0), f1 = min(upto, r1 - 1);
     if (f1 >= f0) {
       const int nf = (f1 - f0 + 1) * g.C * g.W;
-      for (int t = threadIdx.x; t < nf; t += blockDim.x) {
+      // CIMQ_FOLD_XB elements per thread and round, their x loads issued together ahead of the sums
+      auto fidx = [&](int t) {
+        const int iw = t & (g.W - 1), rest = t >> v.lwin;
+        const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
+        const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
+        return (((size_t)b * g.C + c) * g.H + ih) * g.W + iw;
+      };
+      for (int t0 = threadIdx.x; t0 < nf; t0 += CIMQ_FOLD_XB * blockDim.x) {
+      float xb[CIMQ_FOLD_XB];
+#pragma unroll
+      for (int u = 0; u < CIMQ_FOLD_XB; ++u) {
+        const int t = t0 + u * (int)blockDim.x;
+        xb[u] = (LSQ && t < nf) ? x[fidx(t)] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CIMQ_FOLD_XB; ++u) {
+        const int t = t0 + u * (int)blockDim.x;
+        if (t >= nf) break;
         const int iw = t & (g.W - 1), rest = t >> v.lwin;  // power-of-two W (v7_plan)
         const int c = v.lcin >= 0 ? (rest & (g.C - 1)) : rest % g.C;
         const int ih = f0 + (v.lcin >= 0 ? (rest >> v.lcin) : rest / g.C);
@@ -351,7 +372,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
         const float gqv = a * scale;
         if (LSQ) {
           // autograd of round_pass(clamp(x/sa, 0, Qp)) * sa (lsq.py:549), as cim_bwd_gx_v6_kernel
-          const float xv = x[gi];
+          const float xv = xb[u];
           const float y1 = xv / sa;
           const float clv = clamp_nan(y1, 0.f, g.lsq_qp);
           const float rr2 = rintf(clv);
@@ -366,6 +387,7 @@ __global__ __launch_bounds__(256 * NPART) void cim_bwd_gx_v8_kernel(Geo g, V7 v,
         } else {
           gx[gi] = gqv;
         }
+      }
       }
       done = f1;
     }
@@ -694,8 +716,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
                 const uint32_t sgn = (ngw[e] << (31 - kk)) & 0x80000000u;
                 q += __uint_as_float((__float_as_uint(gv[e]) ^ sgn) & nzm);
               }
-              q += __shfl_xor(q, 16);
-              q += __shfl_xor(q, 32);
+              q = rows4_sum(q);
               if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
             }
           }
@@ -782,8 +803,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
             for (int kj = 0; kj < NKJ; ++kj) {
               float q = qv[kj];
-              q += __shfl_xor(q, 16);
-              q += __shfl_xor(q, 32);
+              q = rows4_sum(q);
               if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
             }
           }
@@ -842,8 +862,7 @@ __global__ __launch_bounds__(256, 2) void cim_bwd_gw_v7_kernel(Geo g, V7 v, cons
 #pragma unroll
         for (int kj = 0; kj < NGQ; ++kj) {
           float q = tl == 0 ? gq0[kj] : gq1[kj];
-          q += __shfl_xor(q, 16);
-          q += __shfl_xor(q, 32);
+          q = rows4_sum(q);
           if (g4 == 0) red[((wave * NTL + tl) * NKJ + kj) * 16 + r16] += q;
         }
       }

@@ -30,6 +30,11 @@ VARIANTS = {
     "f_nostage": ["CIMQ_EXP_F_NOSTAGE"],
     "f_nogxgw": ["CIMQ_EXP_F_NOGX", "CIMQ_EXP_F_NOGW"],
     "c1_nopairs": ["CIMQ_EXP_C1_NOPAIRS"],
+    "f_pf2": ["CIMQ_EXP_F_PF2"],
+    "c1_ldsadd": ["CIMQ_EXP_C1_LDSADD"],  # round 6: c1's grad_alpha sums as no-return LDS adds
+    "c1_xpf": ["CIMQ_EXP_C1_XPF"],  # round 6: c1's fold x loaded at the step's start
+    "fold_xb4": ["CIMQ_FOLD_XB=4"],  # round 6: the grad_x folds' x loads four elements per thread at a time
+    "c1_both": ["CIMQ_EXP_C1_LDSADD", "CIMQ_EXP_C1_XPF"],  # round 6: the fused grad_x's weight blocks two (c, kh)-blocks ahead
     # forward staging: the weight side (fragments + ADC parameters per tile) / the activation rows
     "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],
     "fwd_nostagex": ["CIMQ_EXP_FWD_NOSTAGEX"],
