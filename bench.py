@@ -48,7 +48,8 @@ RECOMPUTE = os.environ.get("CIMQ_BENCH_RECOMPUTE", "0") == "1"
 TRAFFIC_JSON = os.environ.get("CIMQ_TRAFFIC_JSON", os.path.join(REPO, "profiles", "r06_final", "pmc_traffic.json"))
 # the kernel families the roofline is reported for (libcimq profiler ids) and their rocprof symbol
 # prefixes (the keys of pmc_traffic.json); every launch of a family is timed, all its instantiations
-FAMILIES = {"fwd_v7": ("cimq::cim_fwd_v3_kernel<", "cimq::cim_fwd5_kernel"), "bwd_fused": "cimq::cim_bwd_fused_kernel<",
+FAMILIES = {"fwd_v7": ("cimq::cim_fwd_v3_kernel<", "cimq::cim_fwd5_kernel"),
+            "bwd_fused": ("cimq::cim_bwd_fused_kernel<", "cimq::cim_bwd_gxw5_kernel"),
             "gx_v8": ("cimq::cim_bwd_gx_v8_kernel<", "cimq::cim_bwd_gx5_kernel"), "gw_v7": ("cimq::cim_bwd_gw_v7_kernel<", "cimq::cim_bwd_gw5_kernel")}
 
 

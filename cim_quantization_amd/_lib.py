@@ -76,8 +76,8 @@ KERNEL_IDS = {"fwd": 1, "bwd_gx": 2, "bwd_gw": 3, "prep_act": 4, "fwd_v7": 5, "g
 # ids 1-4 time every launch of a role (all kernel variants); 5-7 only the v7-path kernels, one
 # rocprof symbol family each (the <NBW, NBA, ...> instantiation the workload uses)
 KERNEL_SYMBOLS = {1: "cim_fwd_*", 2: "cim_bwd_gx_*", 3: "cim_bwd_gw_*", 4: "prep_act_kernel",
-                  5: "cim_fwd_v3_kernel<*, *, *, *> + cim_fwd5_kernel", 6: "cim_bwd_gx_v8_kernel<*, *, *, *, *, *>",
-                  7: "cim_bwd_gw_v7_kernel<*, *, *> + cim_bwd_gw5_kernel", 8: "cim_bwd_fused_kernel<*, *, *>"}
+                  5: "cim_fwd_v3_kernel<*, *, *, *> + cim_fwd5_kernel", 6: "cim_bwd_gx_v8_kernel<*, *, *, *, *, *> + cim_bwd_gx5_kernel",
+                  7: "cim_bwd_gw_v7_kernel<*, *, *> + cim_bwd_gw5_kernel", 8: "cim_bwd_fused_kernel<*, *, *> + cim_bwd_gxw5_kernel<*, *, *> (grad_x and grad_w in one launch)"}
 
 
 class ConvDesc(ctypes.Structure):

@@ -38,7 +38,9 @@ int launch_gxw5(const Geo& g, const PlanX5& px, const PlanG5& pw, const uint8_t*
   const size_t lds = std::max(px.lds, pw.lds);
   CIMQ_TRY(set_lds(kern, lds));
   const int ngw = pw.v.nchunks * pw.pairs;
-  const int slot = prof_begin(KID_GX_V8, g, s);
+  // timed as the fused family (grad_x + grad_w of the layer in one launch: its algorithmic bytes are read gy
+  // and x once, write gx; its MFMA work both contractions), not as grad_x alone
+  const int slot = prof_begin(KID_FUSED, g, s);
   hipLaunchKernelGGL(kern, dim3(px.nblk + ngw), dim3(512), lds, s, g, px.v, vw, reinterpret_cast<const uint32_t*>(ctx + L.st),
                      reinterpret_cast<const v4i*>(wreg(g, ctx) + L.wg5), params_of(g, const_cast<uint8_t*>(ctx)), sw, sa,
                      gout, x, gx, reinterpret_cast<float*>(ws + W.lsq_part), reinterpret_cast<const uint32_t*>(ctx + L.xhat),

@@ -31,9 +31,13 @@ VARIANTS = {
     "f_nogxgw": ["CIMQ_EXP_F_NOGX", "CIMQ_EXP_F_NOGW"],
     "c1_nopairs": ["CIMQ_EXP_C1_NOPAIRS"],
     "f_pf2": ["CIMQ_EXP_F_PF2"],
-    "c1_ldsadd": ["CIMQ_EXP_C1_LDSADD"],  # round 6: c1's grad_alpha sums as no-return LDS adds
-    "c1_xpf": ["CIMQ_EXP_C1_XPF"],  # round 6: c1's fold x loaded at the step's start
+    "c1_ldsadd": ["CIMQ_EXP_C1_LDSADD"],  # round 6: c1's grad_alpha sums as no-return LDS adds (slower: not kept)
+    "c1_xpf": ["CIMQ_EXP_C1_XPF"],  # round 6: c1's fold x loaded at the step's start (neutral: not kept)
     "fold_xb4": ["CIMQ_FOLD_XB=4"],  # round 6: the grad_x folds' x loads four elements per thread at a time
+    "f_cbu2": ["CIMQ_EXP_F_CBU2"],  # round 6: the fused grad_x's (c, kh)-block loop unrolled by two (-0.8 us: not kept)
+    "c1_sb2": ["CIMQ_EXP_C1_SB2"],  # round 6: c1's scheduling fence after every second slice (+1 us: not kept)
+    "gxw5_il": ["CIMQ_EXP_GXW5_ORDER=1"],  # round 6: the merged launch's two roles interleaved (slower: not kept)
+    "gxw5_wf": ["CIMQ_EXP_GXW5_ORDER=2"],  # round 6: grad_w's workgroups first (slower: not kept)
     "c1_both": ["CIMQ_EXP_C1_LDSADD", "CIMQ_EXP_C1_XPF"],  # round 6: the fused grad_x's weight blocks two (c, kh)-blocks ahead
     # forward staging: the weight side (fragments + ADC parameters per tile) / the activation rows
     "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],

@@ -12,8 +12,8 @@ steps = []
 for a, b in zip(marks, marks[1:]):
     wall = int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b])
-    # a training step launches 58 kernels (the forward-only graph windows: 38-40)
-    if busy > 0.95 * wall and b - a > 50:
+    # a training step's window holds backward kernels (the forward-only graph windows do not)
+    if busy > 0.95 * wall and any("cim_bwd_" in r["Kernel_Name"] for r in rows[a:b]):
         steps.append((a, b, wall))
 d = collections.defaultdict(float)
 cnt = collections.defaultdict(int)
