@@ -38,6 +38,10 @@ VARIANTS = {
     "c1_sb2": ["CIMQ_EXP_C1_SB2"],  # round 6: c1's scheduling fence after every second slice (+1 us: not kept)
     "gxw5_il": ["CIMQ_EXP_GXW5_ORDER=1"],  # round 6: the merged launch's two roles interleaved (slower: not kept)
     "gxw5_wf": ["CIMQ_EXP_GXW5_ORDER=2"],  # round 6: grad_w's workgroups first (slower: not kept)
+    "gx5_noploop": ["CIMQ_EXP_GX5_NOPLOOP"],  # round 6: gx5 without its A reads and MFMAs (timing only)
+    "gx5_nosync": ["CIMQ_EXP_GX5_NOSYNC"],  # round 6: gx5 without its step barriers (timing only)
+    "gx5_noepi": ["CIMQ_EXP_GX5_NOEPI"],  # round 6: gx5 without the per-m-tile x read / gx store (timing only)
+    "gx5_bare": ["CIMQ_EXP_GX5_NOPLOOP", "CIMQ_EXP_GX5_NOBUILD", "CIMQ_EXP_GX5_NOLOAD", "CIMQ_EXP_GX5_NOEPI"],
     "c1_both": ["CIMQ_EXP_C1_LDSADD", "CIMQ_EXP_C1_XPF"],  # round 6: the fused grad_x's weight blocks two (c, kh)-blocks ahead
     # forward staging: the weight side (fragments + ADC parameters per tile) / the activation rows
     "fwd_nostagew": ["CIMQ_EXP_FWD_NOSTAGEW"],
