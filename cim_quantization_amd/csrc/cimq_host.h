@@ -910,7 +910,10 @@ inline PlanX5 x5_plan_compute(const Geo& g) {
   // 32-bit element / state-word offsets in the kernel
   if ((long long)g.T * g.M * g.O >= (1LL << 31) || (long long)g.Nin >= (1LL << 31) || (long long)g.M * g.O >= (1LL << 31))
     return p;
-  p.nblk = std::min(p.v.nmt, tune("GX5_GRID", 512));
+  // 256 workgroups (one per CU) since grad_x and grad_w share a launch: grad_w's workgroups then start beside
+  // grad_x's instead of behind them (whole step 2.30 -> 2.28 ms, 4 of 4 A/B pairs; 512 was best for gx5
+  // alone; 128 / 192 / 320 / 384 / 768 / 1024 slower: profiles/r06_final/extra/gxw5_grid_sweep.txt)
+  p.nblk = std::min(p.v.nmt, tune("GX5_GRID", 256));
   p.lds = (size_t)3 * 6 * (g.W + 2) * 96 + 32 + (size_t)9 * 2 * p.v.CBN * 1024 + 32 * 4;
   p.ok = p.lds <= (size_t)80 * 1024;
   return p;
