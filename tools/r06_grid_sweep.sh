@@ -9,6 +9,18 @@ run() {  # name, env...
     --no-cfg5 --no-peaks > gpurun_out/r06_grid/$n.json 2> gpurun_out/r06_grid/$n.err || exit 1
   echo "$n $(python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['ms_per_step'],4))" gpurun_out/r06_grid/$n.json)"
 }
+if [ "$1" = "3" ]; then  # the forward's grid (FWD5_GRID: workgroups per output-block group; NOB2: two output blocks per
+  # 1024-thread workgroup), with grad_x's 256 workgroups as the sources now default to
+run f_d1 CIMQ_TUNE_GX5_GRID=256
+run f_g384 CIMQ_TUNE_GX5_GRID=256 CIMQ_TUNE_FWD5_GRID=384
+run f_g512 CIMQ_TUNE_GX5_GRID=256 CIMQ_TUNE_FWD5_GRID=512
+run f_nob1 CIMQ_TUNE_GX5_GRID=256 CIMQ_TUNE_FWD5_NOB2=0
+run f_d2 CIMQ_TUNE_GX5_GRID=256
+run f_g192 CIMQ_TUNE_GX5_GRID=256 CIMQ_TUNE_FWD5_GRID=192
+run f_g768 CIMQ_TUNE_GX5_GRID=256 CIMQ_TUNE_FWD5_GRID=768
+run f_d3 CIMQ_TUNE_GX5_GRID=256
+exit 0
+fi
 if [ "$1" = "2" ]; then
 run d1 X=0
 run gx256a CIMQ_TUNE_GX5_GRID=256
